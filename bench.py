@@ -1,0 +1,345 @@
+#!/usr/bin/env python3
+"""Benchmark of the libbrb_core/crypto hot path on MI355X (BASELINE.json metric).
+
+Default workload (N = 1): BASELINE config 2 -- 65 536 records x 1500 B, MD5 digest of every record
+through BRB_MD5BatchFixed (device mode), inputs resident in HBM.  One "step" = one pass of the hot
+path over one batch.  With N GPUs every rank digests its own 65 536-record shard of a global
+N x 65 536-record batch (record sharding, no collective on the data path): weak scaling.
+
+Honesty rules applied here:
+  * each step reads a batch the previous R-1 steps did not touch (R rotation buffers totalling
+    >= 640 MB > the 256 MiB Infinity Cache), so the kernel streams from HBM, not from L3;
+  * the timed region is K back-to-back steps between barrier + synchronize on both sides; value is
+    the whole-job rate (all ranks' bytes / max over ranks of the wall time);
+  * roofline.achieved uses the kernel's own average duration from HIP events recorded on the
+    stream the kernel runs on; digests of the last step are spot-checked against hashlib.
+
+Other workloads for DESIGN.md: --config 3 (1 Mi x 64 B MD5), --config 4 (1 GiB Blowfish enc+dec),
+--op sha1.  Run `python bench.py --help`.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s (device-resident) + Mrecords/s over 1500B buffers at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+L3_BYTES = 256 << 20
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--op", default="md5", choices=["md5", "sha1"])
+    ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-inclusive (PCIe) measurement")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
+    return ap.parse_args()
+
+
+def relaunch_distributed(args) -> None:
+    """`python bench.py --gpus N` outside torchrun: start torchrun as a child (no exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000), __file__] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def cpu_threads() -> int:
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        if os.environ.get(var, "").isdigit():
+            return max(1, int(os.environ[var]))
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def load_traffic(path, key):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "RANK" not in os.environ:
+        relaunch_distributed(args)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    if not brb.gpu_available():
+        raise SystemExit("libbrb_crypto_gpu: " + brb.lib().BRB_CryptoGPU_LastError().decode())
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def log(msg):
+        if rank == 0:
+            print(msg, file=sys.stderr, flush=True)
+
+    cfg_id = args.config
+    cfg = workload.CONFIGS[cfg_id]
+    stream = torch.cuda.current_stream(dev)
+
+    if cfg["op"] == "blowfish":
+        result = bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
+    else:
+        result = bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------------
+def timed_steps(launch, n_steps, stream, barrier, max_over_ranks, torch):
+    """K steps between barrier+sync; per-launch HIP events on the launch stream."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(n_steps):
+        ev[k][0].record(stream)
+        launch(k)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return max_over_ranks(wall), sorted(kern_ms)
+
+
+def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log):
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+
+    L = cfg["rec_len"]
+    if cfg_id == 5:
+        n_rank = workload.CONFIGS[5]["records"] // 8          # one GPU's shard of cfg5
+    else:
+        n_rank = cfg["records"]
+    if args.records_per_gpu:
+        n_rank = args.records_per_gpu
+    n_global = n_rank * world
+    r0 = rank * n_rank                                         # this rank's contiguous shard
+    seed = workload.SEEDS[cfg_id]
+    fn = brb.md5_batch_fixed if args.op == "md5" else brb.sha1_batch_fixed
+    width = 16 if args.op == "md5" else 20
+
+    t = time.perf_counter()
+    host = workload.gen_records(seed, r0, n_rank, L)
+    log(f"[bench] generated {host.nbytes / 1e6:.1f} MB on host in {time.perf_counter() - t:.1f}s")
+    batch_bytes = host.nbytes
+    n_rot = max(2, math.ceil(640e6 / batch_bytes)) if batch_bytes < 2.5 * L3_BYTES else 1
+    bufs = [torch.from_numpy(host).to(dev)]
+    for _ in range(n_rot - 1):
+        bufs.append(bufs[0].clone())
+    out = torch.empty((n_rank, width), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+
+    def launch(k):
+        fn(bufs[k % n_rot], L, n_rank, out=out, stream=stream, async_=True)
+
+    for k in range(args.warmup):
+        launch(k)
+    torch.cuda.synchronize()
+    wall, kern_ms = timed_steps(lambda k: launch(k + args.warmup), args.steps, stream, barrier, max_over_ranks, torch)
+
+    # spot-check the last step's digests against hashlib (stdlib, independent of this repo)
+    got = out.cpu().numpy()
+    h = hashlib.md5 if args.op == "md5" else hashlib.sha1
+    for i in list(np.random.default_rng(rank).integers(0, n_rank, 32)) + [0, n_rank - 1]:
+        assert got[i].tobytes() == h(host[i * L:(i + 1) * L].tobytes()).digest(), f"digest mismatch at {i}"
+
+    total_bytes = n_global * L * args.steps
+    gib_s = total_bytes / wall / 2**30
+    mrec_s = n_global * args.steps / wall / 1e6
+    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+    med_kern_s = kern_ms[len(kern_ms) // 2] / 1e3
+    achieved = n_rank * L / avg_kern_s / 1e9
+    traffic = load_traffic(args.pmc_summary, f"cfg{cfg_id}_{args.op}")
+    result = {
+        "metric": METRIC,
+        "value": round(gib_s, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (SURVEY §8(d) splitmix64 generator, HBM-resident, L3-defeating rotation of "
+                f"{n_rot} copies)",
+        "config": {"workload": cfg["name"] + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else ""),
+                   "op": f"{'BRB_MD5BatchFixed' if args.op == 'md5' else 'BrbSha1_BatchFixed'} (device mode)",
+                   "records_per_gpu": n_rank, "record_bytes": L, "global_records": n_global,
+                   "parallelism": f"record-shard x{world}, no collective"},
+        "mrecords_per_s": round(mrec_s, 3),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel_us_avg": round(avg_kern_s * 1e6, 2), "kernel_us_median": round(med_kern_s * 1e6, 2),
+                     "bytes_per_launch": n_rank * L},
+    }
+    if world == 1 and not args.no_pcie:
+        result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, dev, stream, log)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_digest(args, host, L, n_rank, log)
+    log(f"[bench] kernel avg {avg_kern_s * 1e6:.1f} us -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.1%} of HBM peak)")
+    return result
+
+
+def bench_pcie_digest(fn, host, L, n, width, dev, stream, log):
+    """Host-inclusive rate: inputs in pinned host memory, digests back to host, through the host
+    mode of the C ABI (one call = H2D + kernel + D2H, synchronous)."""
+    import numpy as np
+    import torch
+    pinned = torch.from_numpy(host).pin_memory()
+    out = np.empty((n, width), np.uint8)
+    hp = pinned.numpy()
+    fn(hp, L, n, out=out)                       # warm the workspace
+    reps = 5
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn(hp, L, n, out=out)
+    dt = (time.perf_counter() - t) / reps
+    return {"gib_s": round(host.nbytes / dt / 2**30, 2), "ms_per_batch": round(dt * 1e3, 3),
+            "note": "pinned host input -> H2D -> kernel -> D2H digests, synchronous host-mode call"}
+
+
+def cpu_baseline_digest(args, host, L, n, log):
+    import oracle     # test infrastructure: the CPU restatement is the baseline, never the product
+    threads = cpu_threads()
+    fn = oracle.md5_batch_fixed if args.op == "md5" else oracle.sha1_batch_fixed
+    res = {}
+    for th in (threads, 1):
+        n_s = n if th > 1 else max(1, n // 16)
+        fn(host, L, min(n_s, 1024), threads=th)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            fn(host, L, n_s, threads=th)
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds / 2:
+                break
+        dt = time.perf_counter() - t0
+        res[th] = (n_s * L * reps / dt / 2**30, reps, n_s)
+    gib, reps, n_s = res[threads]
+    log(f"[bench] cpu baseline {gib:.2f} GiB/s on {threads} threads, {res[1][0]:.3f} GiB/s on 1")
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/brb_oracle.c {args.op} over the same {n_s} x {L} B records, {reps} passes, "
+                      f"{threads} pthreads (-O2 as libbrb_core/Makefile.linux:3)",
+            "single_core_gib_s": round(res[1][0], 4)}
+
+
+# ------------------------------------------------------------------------------------------------
+def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log):
+    """cfg4: 65 536 x 16 KiB records, Blowfish encrypt then decrypt (one ctx), per GPU."""
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+    import oracle
+
+    n_rec = args.records_per_gpu or cfg["records"]
+    n_words = n_rec * cfg["rec_len"] // 8
+    n_blocks = n_words // 2
+    ctx = brb.blowfish_init(workload.CFG4_KEY)
+    cdev = torch.frombuffer(bytearray(brb.blowfish_ctx_bytes(ctx)), dtype=torch.uint8).to(dev)
+    t = time.perf_counter()
+    w = workload.gen_words(workload.SEEDS[4], n_words, r0=rank * n_words)
+    log(f"[bench] generated {w.nbytes / 1e6:.0f} MB of plaintext in {time.perf_counter() - t:.1f}s")
+    d = torch.from_numpy(w.view(np.int64)).to(dev)
+    d0 = d.clone()
+    ev_enc = []
+
+    def launch(k):
+        brb.blowfish_encrypt_batch(cdev, d, n_blocks, stream=stream, async_=True)
+        brb.blowfish_decrypt_batch(cdev, d, n_blocks, stream=stream, async_=True)
+
+    for k in range(args.warmup):
+        launch(k)
+    torch.cuda.synchronize()
+    wall, kern_ms = timed_steps(launch, args.steps, stream, barrier, max_over_ranks, torch)
+    assert torch.equal(d, d0), "Blowfish round trip did not restore the plaintext"
+    # one encrypt-only check against the oracle on a sample record
+    brb.blowfish_encrypt_batch(cdev, d, n_blocks)
+    wpr = cfg["rec_len"] // 8
+    got = d[:wpr].cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, oracle.bf_ecb(oracle.bf_init(workload.CFG4_KEY), w[:wpr].copy()))
+    step_s = sum(kern_ms) / len(kern_ms) / 1e3
+    plain = n_words * 8
+    result = {
+        "metric": "GiB/s of plaintext per Blowfish encrypt+decrypt round trip (cfg4)",
+        "value": round(plain * world * args.steps / wall / 2**30, 2),
+        "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (splitmix64 words, HBM-resident)",
+        "config": {"workload": cfg["name"], "records_per_gpu": n_rec, "record_bytes": cfg["rec_len"],
+                   "parallelism": f"record-shard x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(4 * plain / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(4 * plain / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic(args.pmc_summary, "cfg4_blowfish"),
+                     "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": 4 * plain,
+                     "note": "algorithmic bytes = read + write of the plaintext in each direction"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        oc = oracle.bf_init(workload.CFG4_KEY)
+        th = cpu_threads()
+        sample = w[: min(n_words, 2 * 1024 * 1024)].copy()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            oracle.bf_ecb(oc, sample, threads=th)
+            oracle.bf_ecb(oc, sample, decrypt=True, threads=th)
+            reps += 1
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": round(sample.nbytes * reps / dt / 2**30, 3), "unit": "GiB/s",
+                                  "cores": th, "kind": "port",
+                                  "sample": f"oracle bf_ecb enc+dec over {sample.nbytes >> 20} MiB, {reps} passes"}
+    return result
+
+
+if __name__ == "__main__":
+    main()

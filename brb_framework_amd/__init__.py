@@ -1,0 +1,39 @@
+"""brb_framework_amd -- MI355X-native libbrb_core/crypto (MD5, SHA-1, 64-bit-word Blowfish).
+
+The product is the C-ABI shared library ``libbrb_crypto_gpu.so`` built in this directory
+(``make -C brb_framework_amd``); its interface is ``include/brb_crypto.h``.  This Python package is
+plumbing for tests and benchmarks: it loads that library with ctypes and exposes its entry points
+with the reference's names (``BRB_MD5Init`` ... ``BRB_Blowfish_Decrypt``) plus thin helpers for the
+batch surface that accept numpy arrays (host mode) or torch CUDA tensors (device mode).
+
+Nothing here computes a digest or a cipher in Python, and nothing falls back to the CPU: if the
+library is missing, ``lib()`` raises; if no GPU is usable, the batch helpers raise ``RuntimeError``
+with the library's own reason.
+"""
+from .crypto import (  # noqa: F401
+    BATCH_ASYNC,
+    BATCH_DEVICE,
+    BATCH_HOST,
+    BRB_BLOWFISH_CTX,
+    BRB_MD5_CTX,
+    BrbSha1Ctx,
+    LIB_PATH,
+    blowfish_ctx_bytes,
+    blowfish_decrypt_batch,
+    blowfish_encrypt_batch,
+    blowfish_init,
+    exported_symbols,
+    gpu_available,
+    lib,
+    md5_batch,
+    md5_batch_fixed,
+    sha1_batch,
+    sha1_batch_fixed,
+)
+
+__all__ = [
+    "BATCH_ASYNC", "BATCH_DEVICE", "BATCH_HOST", "BRB_BLOWFISH_CTX", "BRB_MD5_CTX", "BrbSha1Ctx",
+    "LIB_PATH", "blowfish_ctx_bytes", "blowfish_decrypt_batch", "blowfish_encrypt_batch",
+    "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
+    "sha1_batch", "sha1_batch_fixed",
+]

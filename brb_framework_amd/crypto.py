@@ -1,0 +1,230 @@
+"""ctypes binding of libbrb_crypto_gpu.so (include/brb_crypto.h).  Test/bench plumbing only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbrb_crypto_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "brb_crypto.h")
+
+BATCH_HOST = 0x0
+BATCH_DEVICE = 0x1
+BATCH_ASYNC = 0x2
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+ulp = ctypes.POINTER(ctypes.c_ulong)
+
+
+class BRB_MD5_CTX(ctypes.Structure):
+    """libbrb_data.h:854-860"""
+    _fields_ = [("buf", ctypes.c_uint32 * 4), ("bytes", ctypes.c_uint32 * 2), ("in_", ctypes.c_uint32 * 16),
+                ("digest", ctypes.c_ubyte * 16), ("string", ctypes.c_ubyte * 64)]
+
+
+class BrbSha1Ctx(ctypes.Structure):
+    """libbrb_data.h:1937-1943"""
+    _fields_ = [("state", ctypes.c_uint32 * 5), ("count", ctypes.c_uint32 * 2), ("buffer", ctypes.c_uint8 * 64)]
+
+
+class BRB_BLOWFISH_CTX(ctypes.Structure):
+    """libbrb_data.h:876-879 (LP64: unsigned long = 8 bytes)"""
+    _fields_ = [("P", ctypes.c_ulong * 18), ("S", (ctypes.c_ulong * 256) * 4)]
+
+
+assert ctypes.sizeof(BRB_MD5_CTX) == 168 and ctypes.sizeof(BrbSha1Ctx) == 92
+assert ctypes.sizeof(BRB_BLOWFISH_CTX) == 8336
+
+_LIB = None
+
+# (name, restype, argtypes) of every function include/brb_crypto.h declares
+_SIGNATURES = [
+    ("BRB_MD5Init", None, [ctypes.POINTER(BRB_MD5_CTX)]),
+    ("BRB_MD5UpdateBig", None, [ctypes.POINTER(BRB_MD5_CTX), ctypes.c_void_p, ctypes.c_ulong]),
+    ("BRB_MD5Update", None, [ctypes.POINTER(BRB_MD5_CTX), ctypes.c_void_p, ctypes.c_ulong]),
+    ("BRB_MD5UpdateLowerText", None, [ctypes.POINTER(BRB_MD5_CTX), ctypes.c_char_p, ctypes.c_int]),
+    ("BRB_MD5Final", None, [ctypes.POINTER(BRB_MD5_CTX)]),
+    ("BRB_MD5Transform", None, [ctypes.POINTER(BRB_MD5_CTX)]),
+    ("BRB_MD5LateInitDigestString", None, [ctypes.POINTER(BRB_MD5_CTX)]),
+    ("BRB_MD5ToStr", None, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("BrbSha1_Init", None, [ctypes.POINTER(BrbSha1Ctx)]),
+    ("BrbSha1_Update", None, [ctypes.POINTER(BrbSha1Ctx), ctypes.c_void_p, ctypes.c_size_t]),
+    ("BrbSha1_Final", None, [ctypes.POINTER(BrbSha1Ctx), ctypes.c_void_p]),
+    ("BrbSha1_Transform", None, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("BrbSha1_Do", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    ("BRB_Blowfish_Init", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ctypes.c_void_p, ctypes.c_int]),
+    ("BRB_Blowfish_Encrypt", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ulp, ulp]),
+    ("BRB_Blowfish_Decrypt", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ulp, ulp]),
+    ("BRB_MD5BatchFixed", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_MD5Batch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint,
+      ctypes.c_void_p]),
+    ("BrbSha1_BatchFixed", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    ("BrbSha1_Batch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint,
+      ctypes.c_void_p]),
+    ("BRB_Blowfish_EncryptBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_Blowfish_DecryptBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_CryptoGPU_Available", ctypes.c_int, []),
+    ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
+    ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
+]
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree library; raise if it has not been built (no silent fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {HERE}` "
+                               "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def exported_symbols() -> set:
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], check=True, capture_output=True, text=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+def gpu_available() -> bool:
+    return bool(lib().BRB_CryptoGPU_Available())
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 1:
+        msg = lib().BRB_CryptoGPU_LastError().decode(errors="replace")
+        raise RuntimeError(f"{what} returned {rc}: {msg}")
+
+
+# ---- buffer helpers ---------------------------------------------------------------------------
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if _is_torch(x):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return x.ctypes.data
+    raise TypeError(f"unsupported buffer type {type(x)}")
+
+
+def _mode(data, stream, async_):
+    """(flags, stream_handle) for a buffer: torch CUDA tensor -> device mode, numpy -> host mode."""
+    if _is_torch(data):
+        if not data.is_cuda:
+            raise ValueError("torch tensors must live on a CUDA (HIP) device; pass numpy for host mode")
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(data.device)
+        handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+        return BATCH_DEVICE | (BATCH_ASYNC if async_ else 0), handle
+    return BATCH_HOST, (int(stream) if stream is not None else 0)
+
+
+def _out_like(data, n, width):
+    if _is_torch(data):
+        import torch
+        return torch.empty((n, width), dtype=torch.uint8, device=data.device)
+    return np.empty((n, width), dtype=np.uint8)
+
+
+def _nbytes(x) -> int:
+    return x.numel() * x.element_size() if _is_torch(x) else x.nbytes
+
+
+def _digest_fixed(fn, width, data, rec_len, n, out, stream, async_):
+    if n is None:
+        n = _nbytes(data) // rec_len if rec_len else 0
+    if rec_len * n > _nbytes(data):
+        raise ValueError("data is smaller than rec_len * n")
+    if out is None:
+        out = _out_like(data, n, width)
+    flags, h = _mode(data, stream, async_)
+    _check(fn(_ptr(data), rec_len, n, _ptr(out), flags, h), fn.__name__)
+    return out
+
+
+def _digest_var(fn, width, data, offsets, lengths, out, stream, async_):
+    n = len(offsets)
+    if out is None:
+        out = _out_like(data, n, width)
+    flags, h = _mode(data, stream, async_)
+    _check(fn(_ptr(data), _ptr(offsets), _ptr(lengths), n, _ptr(out), flags, h), fn.__name__)
+    return out
+
+
+def md5_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False):
+    """BRB_MD5BatchFixed: digests (n, 16) of n records of rec_len bytes stored back to back."""
+    return _digest_fixed(lib().BRB_MD5BatchFixed, 16, data, rec_len, n, out, stream, async_)
+
+
+def sha1_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False):
+    """BrbSha1_BatchFixed: digests (n, 20)."""
+    return _digest_fixed(lib().BrbSha1_BatchFixed, 20, data, rec_len, n, out, stream, async_)
+
+
+def md5_batch(data, offsets, lengths, out=None, stream=None, async_=False):
+    """BRB_MD5Batch: offsets uint64[n], lengths uint32[n] (same memory kind as data)."""
+    return _digest_var(lib().BRB_MD5Batch, 16, data, offsets, lengths, out, stream, async_)
+
+
+def sha1_batch(data, offsets, lengths, out=None, stream=None, async_=False):
+    return _digest_var(lib().BrbSha1_Batch, 20, data, offsets, lengths, out, stream, async_)
+
+
+# ---- Blowfish ------------------------------------------------------------------------------------
+def blowfish_init(key: bytes, key_len: int | None = None) -> BRB_BLOWFISH_CTX:
+    ctx = BRB_BLOWFISH_CTX()
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    lib().BRB_Blowfish_Init(ctypes.byref(ctx), kb, len(key) if key_len is None else key_len)
+    return ctx
+
+
+def blowfish_ctx_bytes(ctx: BRB_BLOWFISH_CTX) -> bytes:
+    return ctypes.string_at(ctypes.addressof(ctx), ctypes.sizeof(ctx))
+
+
+def _bf(fn, ctx, words, n_blocks, stream, async_):
+    """words: uint64 numpy array (host) or int64/uint64 torch CUDA tensor (device), 2 words per block.
+    ctx: BRB_BLOWFISH_CTX (host mode) or, in device mode, a CUDA uint8 tensor holding its 8336 bytes
+    (a BRB_BLOWFISH_CTX is uploaded for you)."""
+    if n_blocks is None:
+        n_blocks = _nbytes(words) // 16
+    if 16 * n_blocks > _nbytes(words):
+        raise ValueError("words holds fewer than n_blocks (xl, xr) pairs")
+    flags, h = _mode(words, stream, async_)
+    if flags & BATCH_DEVICE:
+        if isinstance(ctx, BRB_BLOWFISH_CTX):
+            import torch
+            ctx = torch.frombuffer(bytearray(blowfish_ctx_bytes(ctx)), dtype=torch.uint8).to(words.device)
+        cptr = _ptr(ctx)
+    else:
+        cptr = ctypes.addressof(ctx)
+    _check(fn(cptr, _ptr(words), n_blocks, flags, h), fn.__name__)
+    return words
+
+
+def blowfish_encrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False):
+    return _bf(lib().BRB_Blowfish_EncryptBatch, ctx, words, n_blocks, stream, async_)
+
+
+def blowfish_decrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False):
+    return _bf(lib().BRB_Blowfish_DecryptBatch, ctx, words, n_blocks, stream, async_)

@@ -1,0 +1,302 @@
+// batch_api.hip -- the exported C ABI of the batch (GPU) surface; see include/brb_crypto.h.
+//
+// Host mode (BRB_BATCH_HOST): inputs are copied into a per-thread device workspace, the kernel
+// runs, results are copied back, and the call returns after the stream has drained.
+// Device mode (BRB_BATCH_DEVICE): the caller's HBM-resident buffers are used in place.
+// There is no CPU fallback anywhere in this file: a missing or failing device returns
+// BRB_BATCH_NOT_DONE with the reason in BRB_CryptoGPU_LastError().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "brb_crypto.h"
+#include "brb_kernels.h"
+
+namespace {
+
+thread_local std::string t_err;
+
+void set_err(const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_err = buf;
+}
+
+int fail_hip(const char *what, hipError_t e)
+{
+    set_err("%s: %s (%d)", what, hipGetErrorString(e), int(e));
+    return BRB_BATCH_NOT_DONE;
+}
+
+int device_ok()
+{
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess)
+        return fail_hip("hipGetDeviceCount", e);
+    if (n <= 0) {
+        set_err("no HIP device visible to this process");
+        return BRB_BATCH_NOT_DONE;
+    }
+    return BRB_BATCH_OK;
+}
+
+// Per-thread, per-device grow-only scratch for host-mode batches.
+struct Workspace {
+    void *ptr = nullptr;
+    size_t cap = 0;
+    int dev = -1;
+};
+thread_local Workspace t_ws;
+
+void *workspace(size_t bytes, hipError_t *err)
+{
+    int dev = 0;
+    *err = hipGetDevice(&dev);
+    if (*err != hipSuccess)
+        return nullptr;
+    if (t_ws.ptr && (t_ws.dev != dev || t_ws.cap < bytes)) {
+        if (t_ws.dev == dev) {
+            (void)hipFree(t_ws.ptr);
+        } else {
+            int cur = dev;
+            (void)hipSetDevice(t_ws.dev);
+            (void)hipFree(t_ws.ptr);
+            (void)hipSetDevice(cur);
+        }
+        t_ws.ptr = nullptr;
+        t_ws.cap = 0;
+    }
+    if (!t_ws.ptr) {
+        size_t cap = std::max<size_t>(bytes, size_t(1) << 20);
+        *err = hipMalloc(&t_ws.ptr, cap);
+        if (*err != hipSuccess) {
+            t_ws.ptr = nullptr;
+            return nullptr;
+        }
+        t_ws.cap = cap;
+        t_ws.dev = dev;
+    }
+    return t_ws.ptr;
+}
+
+inline size_t align_up(size_t x, size_t a)
+{
+    return (x + a - 1) / a * a;
+}
+
+int finish(hipStream_t s, unsigned flags)
+{
+    if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC))
+        return BRB_BATCH_OK;
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess)
+        return fail_hip("hipStreamSynchronize", e);
+    return BRB_BATCH_OK;
+}
+
+using FixedLauncher = hipError_t (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *, hipStream_t);
+using VarLauncher = hipError_t (*)(const uint8_t *, const uint64_t *, const uint32_t *, uint64_t, uint8_t *,
+                                   hipStream_t);
+
+int digest_fixed(FixedLauncher launch, size_t dig_len, const void *data, uint32_t rec_len, uint64_t n_rec,
+                 void *digests, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n_rec == 0)
+        return BRB_BATCH_OK;
+    if (!digests || (!data && rec_len)) {
+        set_err("NULL data or digests");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = launch(static_cast<const uint8_t *>(data), rec_len, n_rec, static_cast<uint8_t *>(digests), s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    const size_t in_bytes = size_t(rec_len) * n_rec;
+    const size_t off_out = align_up(in_bytes, 256);
+    uint8_t *ws = static_cast<uint8_t *>(workspace(off_out + dig_len * n_rec, &e));
+    if (!ws)
+        return fail_hip("device workspace", e);
+    if (in_bytes && (e = hipMemcpyAsync(ws, data, in_bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync H2D", e);
+    if ((e = launch(ws, rec_len, n_rec, ws + off_out, s)) != hipSuccess)
+        return fail_hip("kernel launch", e);
+    if ((e = hipMemcpyAsync(digests, ws + off_out, dig_len * n_rec, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync D2H", e);
+    return finish(s, flags & ~BRB_BATCH_ASYNC);
+}
+
+int digest_var(VarLauncher launch, size_t dig_len, const void *data, const uint64_t *offsets,
+               const uint32_t *lengths, uint64_t n_rec, void *digests, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n_rec == 0)
+        return BRB_BATCH_OK;
+    if (!digests || !offsets || !lengths || !data) {
+        set_err("NULL data, offsets, lengths or digests");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = launch(static_cast<const uint8_t *>(data), offsets, lengths, n_rec, static_cast<uint8_t *>(digests), s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    // host mode: copy the byte range the records cover, rebased to its first byte
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint64_t i = 0; i < n_rec; i++) {
+        if (lengths[i] == 0)
+            continue;
+        lo = std::min(lo, offsets[i]);
+        hi = std::max(hi, offsets[i] + lengths[i]);
+    }
+    if (lo == UINT64_MAX)
+        lo = hi = 0;
+    const size_t span = size_t(hi - lo);
+    const size_t o_off = align_up(span, 256);
+    const size_t o_len = align_up(o_off + 8 * n_rec, 256);
+    const size_t o_dig = align_up(o_len + 4 * n_rec, 256);
+    uint8_t *ws = static_cast<uint8_t *>(workspace(o_dig + dig_len * n_rec, &e));
+    if (!ws)
+        return fail_hip("device workspace", e);
+    uint64_t *rebased = static_cast<uint64_t *>(malloc(8 * n_rec));
+    if (!rebased) {
+        set_err("out of host memory");
+        return BRB_BATCH_NOT_DONE;
+    }
+    for (uint64_t i = 0; i < n_rec; i++)
+        rebased[i] = lengths[i] ? offsets[i] - lo : 0;
+    int rc = BRB_BATCH_OK;
+    if (span && (e = hipMemcpyAsync(ws, static_cast<const uint8_t *>(data) + lo, span, hipMemcpyHostToDevice, s)) != hipSuccess)
+        rc = fail_hip("hipMemcpyAsync H2D", e);
+    else if ((e = hipMemcpyAsync(ws + o_off, rebased, 8 * n_rec, hipMemcpyHostToDevice, s)) != hipSuccess)
+        rc = fail_hip("hipMemcpyAsync H2D", e);
+    else if ((e = hipMemcpyAsync(ws + o_len, lengths, 4 * n_rec, hipMemcpyHostToDevice, s)) != hipSuccess)
+        rc = fail_hip("hipMemcpyAsync H2D", e);
+    else if ((e = launch(ws, reinterpret_cast<const uint64_t *>(ws + o_off), reinterpret_cast<const uint32_t *>(ws + o_len),
+                         n_rec, ws + o_dig, s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    else if ((e = hipMemcpyAsync(digests, ws + o_dig, dig_len * n_rec, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        rc = fail_hip("hipMemcpyAsync D2H", e);
+    if (rc == BRB_BATCH_OK)
+        rc = finish(s, flags & ~BRB_BATCH_ASYNC);
+    else
+        (void)hipStreamSynchronize(s);
+    free(rebased);
+    return rc;
+}
+
+int blowfish_batch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks, unsigned flags,
+                   void *stream, bool decrypt)
+{
+    t_err.clear();
+    if (n_blocks == 0)
+        return BRB_BATCH_OK;
+    if (!ctx || !words) {
+        set_err("NULL ctx or words");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = brb::launch_blowfish(reinterpret_cast<const uint64_t *>(ctx), reinterpret_cast<uint64_t *>(words), n_blocks,
+                                 decrypt, s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    const size_t ctx_bytes = align_up(sizeof(BRB_BLOWFISH_CTX), 256);
+    const size_t w_bytes = size_t(16) * n_blocks;
+    uint8_t *ws = static_cast<uint8_t *>(workspace(ctx_bytes + w_bytes, &e));
+    if (!ws)
+        return fail_hip("device workspace", e);
+    if ((e = hipMemcpyAsync(ws, ctx, sizeof(BRB_BLOWFISH_CTX), hipMemcpyHostToDevice, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync H2D", e);
+    if ((e = hipMemcpyAsync(ws + ctx_bytes, words, w_bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync H2D", e);
+    if ((e = brb::launch_blowfish(reinterpret_cast<const uint64_t *>(ws), reinterpret_cast<uint64_t *>(ws + ctx_bytes),
+                                  n_blocks, decrypt, s)) != hipSuccess)
+        return fail_hip("kernel launch", e);
+    if ((e = hipMemcpyAsync(words, ws + ctx_bytes, w_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync D2H", e);
+    return finish(s, flags & ~BRB_BATCH_ASYNC);
+}
+
+}  // namespace
+
+extern "C" {
+
+int BRB_MD5BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec, unsigned char (*digests)[16], unsigned flags,
+                      void *hip_stream)
+{
+    return digest_fixed(brb::launch_md5_fixed, 16, data, rec_len, n_rec, digests, flags, hip_stream);
+}
+
+int BRB_MD5Batch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n_rec,
+                 unsigned char (*digests)[16], unsigned flags, void *hip_stream)
+{
+    return digest_var(brb::launch_md5_var, 16, data, offsets, lengths, n_rec, digests, flags, hip_stream);
+}
+
+int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec, uint8_t (*digests)[20], unsigned flags,
+                       void *hip_stream)
+{
+    return digest_fixed(brb::launch_sha1_fixed, 20, data, rec_len, n_rec, digests, flags, hip_stream);
+}
+
+int BrbSha1_Batch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n_rec,
+                  uint8_t (*digests)[20], unsigned flags, void *hip_stream)
+{
+    return digest_var(brb::launch_sha1_var, 20, data, offsets, lengths, n_rec, digests, flags, hip_stream);
+}
+
+int BRB_Blowfish_EncryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks, unsigned flags,
+                              void *hip_stream)
+{
+    return blowfish_batch(ctx, words, n_blocks, flags, hip_stream, false);
+}
+
+int BRB_Blowfish_DecryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks, unsigned flags,
+                              void *hip_stream)
+{
+    return blowfish_batch(ctx, words, n_blocks, flags, hip_stream, true);
+}
+
+int BRB_CryptoGPU_Available(void)
+{
+    t_err.clear();
+    return device_ok() == BRB_BATCH_OK ? 1 : 0;
+}
+
+const char *BRB_CryptoGPU_LastError(void)
+{
+    return t_err.c_str();
+}
+
+const char *BRB_CryptoGPU_Version(void)
+{
+    return "brb_crypto_gpu 0.1 (gfx950)";
+}
+
+}  // extern "C"

@@ -1,0 +1,21 @@
+// brb_kernels.h -- internal launchers of the gfx950 crypto kernels (C++ linkage, not exported).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "brb_gpu_common.h"
+
+namespace brb {
+
+// All pointers are device pointers; launches are asynchronous on `s`.
+hipError_t launch_md5_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, hipStream_t s);
+hipError_t launch_md5_var(const uint8_t *data, const uint64_t *offs, const uint32_t *lens, uint64_t n_rec,
+                          uint8_t *out, hipStream_t s);
+hipError_t launch_sha1_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, hipStream_t s);
+hipError_t launch_sha1_var(const uint8_t *data, const uint64_t *offs, const uint32_t *lens, uint64_t n_rec,
+                           uint8_t *out, hipStream_t s);
+// ctx_dev: device copy of BRB_BLOWFISH_CTX (P[18] then S[4][256], 64-bit words)
+hipError_t launch_blowfish(const uint64_t *ctx_dev, uint64_t *words, uint64_t n_blocks, bool decrypt, hipStream_t s);
+
+}  // namespace brb

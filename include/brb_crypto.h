@@ -1,0 +1,143 @@
+/*
+ * brb_crypto.h -- C ABI of libbrb_crypto_gpu.so, the MI355X-native replacement for
+ * libbrb_core/crypto (BrByte brb_framework @ 2024_10_08).
+ *
+ * Two surfaces:
+ *
+ *  1. COMPAT (drop-in): the reference's crypto prototypes with the same names, argument types,
+ *     struct layouts and side effects, so the callers in libbrb_core/comm and libbrb_core/data link
+ *     unchanged (list in INTEGRATION.md).  They run on the calling CPU thread: a single streaming
+ *     context is a serial chain and does not belong on a GPU.
+ *
+ *  2. BATCH (new): many independent records per call, executed by hand-written gfx950 HIP
+ *     kernels.  This is the hot path.  It never falls back to a CPU implementation: if no HIP
+ *     device is usable the call returns 0 and BRB_CryptoGPU_LastError() says why.
+ *
+ * LP64 is assumed, exactly as the reference assumes it (`unsigned long` = 8 bytes inside
+ * BRB_BLOWFISH_CTX).
+ */
+#ifndef BRB_CRYPTO_H
+#define BRB_CRYPTO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ============================================================================================ */
+/* 1. COMPAT SURFACE                                                                              */
+/* ============================================================================================ */
+
+/* ---- MD5 -- replaces libbrb_core/crypto/md5.c; prototypes libbrb_data.h:862-869 ------------ */
+#define MD5_DIGEST_LENGTH 16                      /* libbrb_data.h:852 */
+
+typedef struct _BRB_MD5_CTX {                     /* libbrb_data.h:854-860, sizeof == 168 */
+    uint32_t buf[4];
+    uint32_t bytes[2];
+    uint32_t in[16];
+    unsigned char digest[16];
+    unsigned char string[64];                     /* lowercase hex + NUL after Final */
+} BRB_MD5_CTX;
+
+void BRB_MD5Init(BRB_MD5_CTX *ctx);                                             /* md5.c:38  */
+void BRB_MD5UpdateBig(BRB_MD5_CTX *ctx, const void *_buf, unsigned long len);   /* md5.c:49  */
+void BRB_MD5Update(BRB_MD5_CTX *ctx, const void *_buf, unsigned long len);      /* md5.c:72  */
+/* md5.c:112.  The reference lowercases into a 128-byte stack buffer and overflows it when
+ * key_sz > 128; this version lowercases in 128-byte pieces (same digest, no overflow). */
+void BRB_MD5UpdateLowerText(BRB_MD5_CTX *md5_context, char *key_ptr, int key_sz);
+void BRB_MD5Final(BRB_MD5_CTX *ctx);                                            /* md5.c:134 */
+void BRB_MD5Transform(BRB_MD5_CTX *ctx);                                        /* md5.c:170 */
+void BRB_MD5LateInitDigestString(BRB_MD5_CTX *ret);                             /* md5.c:255 */
+void BRB_MD5ToStr(unsigned char *bin_digest, unsigned char *ret_buf_str);       /* md5.c:264 */
+
+/* ---- SHA-1 -- replaces libbrb_core/crypto/sha1.c; prototypes libbrb_data.h:1947-1951 ------- */
+typedef struct {                                  /* libbrb_data.h:1937-1943, sizeof == 92 */
+    uint32_t state[5];
+    uint32_t count[2];
+    uint8_t buffer[64];
+} BrbSha1Ctx;
+
+#define BRB_SHA1_DIGEST_SIZE 20                   /* libbrb_data.h:1945 */
+
+void BrbSha1_Init(BrbSha1Ctx *context);                                          /* sha1.c:132 */
+/* sha1.c:143.  Like the reference (SHA1HANDSOFF undefined, sha1.c:84-90) every full 64-byte block
+ * transformed directly from `data` is overwritten with message-schedule words W[64..79]. */
+void BrbSha1_Update(BrbSha1Ctx *context, const uint8_t *data, const size_t len);
+void BrbSha1_Final(BrbSha1Ctx *context, uint8_t digest[BRB_SHA1_DIGEST_SIZE]);   /* sha1.c:171 */
+void BrbSha1_Transform(uint32_t state[5], const uint8_t buffer[64]);             /* sha1.c:75  */
+int BrbSha1_Do(const uint8_t *in_ptr, int in_len, char *dig_str);                /* sha1.c:203 */
+
+/* ---- Blowfish -- replaces libbrb_core/crypto/blowfish.c; prototypes libbrb_data.h:881-883 -- */
+typedef struct _BRB_BLOWFISH_CTX {                /* libbrb_data.h:876-879, sizeof == 8336 */
+    unsigned long P[16 + 2];
+    unsigned long S[4][256];
+} BRB_BLOWFISH_CTX;
+
+void BRB_Blowfish_Init(BRB_BLOWFISH_CTX *ctx, unsigned char *key, int keyLen);         /* :382 */
+void BRB_Blowfish_Encrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :312 */
+void BRB_Blowfish_Decrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :347 */
+
+/* ============================================================================================ */
+/* 2. BATCH SURFACE (GPU)                                                                         */
+/* ============================================================================================ */
+
+/* Return codes follow the reference's transform-hook convention (ev_kq_aio_transform.c:52-57):
+ *   1  done
+ *   0  not done: no usable HIP device, device error, or unsupported request
+ *      (BRB_CryptoGPU_LastError() has the reason; nothing was computed on the CPU)
+ *  -1  bad arguments (NULL pointer where one is required, length out of range)         */
+#define BRB_BATCH_OK        1
+#define BRB_BATCH_NOT_DONE  0
+#define BRB_BATCH_BADARG   (-1)
+
+/* flags */
+#define BRB_BATCH_HOST      0x0u   /* pointers are host memory: copied in and out by the call      */
+#define BRB_BATCH_DEVICE    0x1u   /* every pointer (data, offsets, lengths, digests, ctx, words)
+                                      is device memory (HBM-resident); nothing crosses PCIe       */
+#define BRB_BATCH_ASYNC     0x2u   /* with BRB_BATCH_DEVICE: enqueue on `hip_stream` and return
+                                      without waiting; the caller synchronises the stream         */
+
+/* `hip_stream` is a hipStream_t (NULL = the legacy default stream of the current device).
+ * Work runs on the caller's current HIP device (hipSetDevice / torch.cuda.set_device). */
+
+/* MD5 of n_rec records of rec_len bytes each, stored back to back: record i is
+ * data[i*rec_len .. (i+1)*rec_len).  digests[i] = BRB_MD5Init/Update/Final of record i. */
+int BRB_MD5BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec,
+                      unsigned char (*digests)[16], unsigned flags, void *hip_stream);
+
+/* MD5 of n_rec records of arbitrary byte offset and length (record i = data[offsets[i] ..
+ * offsets[i] + lengths[i])).  Records may overlap and need no alignment. */
+int BRB_MD5Batch(const void *data, const uint64_t *offsets, const uint32_t *lengths,
+                 uint64_t n_rec, unsigned char (*digests)[16], unsigned flags, void *hip_stream);
+
+/* SHA-1 batches: digests[i] = BrbSha1_Do(record i) (20 raw big-endian bytes).  Unlike
+ * BrbSha1_Update the batch surface never writes into the input records. */
+int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec,
+                       uint8_t (*digests)[20], unsigned flags, void *hip_stream);
+int BrbSha1_Batch(const void *data, const uint64_t *offsets, const uint32_t *lengths,
+                  uint64_t n_rec, uint8_t (*digests)[20], unsigned flags, void *hip_stream);
+
+/* Blowfish ECB over n_blocks blocks in place.  A block is the reference's (xl, xr) pair of
+ * 64-bit `unsigned long` words (blowfish.c:312, mem_buf.c:1538-1539): words[2i] = xl,
+ * words[2i+1] = xr.  The result equals BRB_Blowfish_Encrypt/Decrypt(ctx, &w[2i], &w[2i+1])
+ * for every i, bit for bit in all 64 bits.  With BRB_BATCH_DEVICE, ctx is a device copy of the
+ * 8336-byte BRB_BLOWFISH_CTX. */
+int BRB_Blowfish_EncryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks,
+                              unsigned flags, void *hip_stream);
+int BRB_Blowfish_DecryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks,
+                              unsigned flags, void *hip_stream);
+
+/* ---- runtime ---------------------------------------------------------------------------- */
+/* 1 if a HIP device is usable from this process, else 0 (reason in LastError). */
+int BRB_CryptoGPU_Available(void);
+/* Last error of the calling thread ("" if none). */
+const char *BRB_CryptoGPU_LastError(void);
+/* Library version string. */
+const char *BRB_CryptoGPU_Version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BRB_CRYPTO_H */

@@ -1,0 +1,170 @@
+"""ctypes binding of the CPU oracle (oracle/brb_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Allowed users: tests/, __graft_entry__.smoke() (as the checker) and bench.py's cpu_baseline leg.
+The product library never imports, links or calls anything in this directory.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+_L = None
+u64 = ctypes.c_uint64
+vp = ctypes.c_void_p
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        sig = {
+            "orc_md5_init": (None, [vp]), "orc_md5_update": (None, [vp, vp, ctypes.c_ulong]),
+            "orc_md5_update_big": (None, [vp, vp, ctypes.c_ulong]), "orc_md5_final": (None, [vp]),
+            "orc_md5": (None, [vp, u64, vp]),
+            "orc_sha1_init": (None, [vp]), "orc_sha1_update": (None, [vp, vp, ctypes.c_size_t]),
+            "orc_sha1_final": (None, [vp, vp]), "orc_sha1": (None, [vp, u64, vp]),
+            "orc_bf_pi_words": (None, [vp]), "orc_bf_init": (None, [vp, vp, ctypes.c_int]),
+            "orc_bf_encrypt": (None, [vp, vp, vp]), "orc_bf_decrypt": (None, [vp, vp, vp]),
+            "orc_bf_ecb": (None, [vp, vp, u64, ctypes.c_int, ctypes.c_int]),
+            "orc_membuf_key": (None, [ctypes.c_uint, vp]),
+            "orc_membuf_encrypt": (u64, [vp, u64, ctypes.c_uint, u64]),
+            "orc_membuf_decrypt": (u64, [vp, u64, ctypes.c_uint, u64]),
+            "orc_md5_batch_fixed": (None, [vp, ctypes.c_uint32, u64, vp, ctypes.c_int]),
+            "orc_sha1_batch_fixed": (None, [vp, ctypes.c_uint32, u64, vp, ctypes.c_int]),
+            "orc_md5_batch": (None, [vp, vp, vp, u64, vp]),
+            "orc_sha1_batch": (None, [vp, vp, vp, u64, vp]),
+            "orc_splitmix64": (u64, [u64]),
+            "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _L = L
+    return _L
+
+
+def _p(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+# ---- digests ----------------------------------------------------------------------------------
+def md5(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(16)
+    lib().orc_md5(data, len(data), out)
+    return out.raw
+
+
+def sha1(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(20)
+    lib().orc_sha1(data, len(data), out)
+    return out.raw
+
+
+def md5_batch_fixed(data: np.ndarray, rec_len: int, n: int, threads: int = 1) -> np.ndarray:
+    out = np.empty((n, 16), np.uint8)
+    lib().orc_md5_batch_fixed(_p(data), rec_len, n, _p(out), threads)
+    return out
+
+
+def sha1_batch_fixed(data: np.ndarray, rec_len: int, n: int, threads: int = 1) -> np.ndarray:
+    out = np.empty((n, 20), np.uint8)
+    lib().orc_sha1_batch_fixed(_p(data), rec_len, n, _p(out), threads)
+    return out
+
+
+def md5_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lengths = np.ascontiguousarray(lengths, np.uint32)
+    out = np.empty((len(offsets), 16), np.uint8)
+    lib().orc_md5_batch(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out))
+    return out
+
+
+def sha1_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lengths = np.ascontiguousarray(lengths, np.uint32)
+    out = np.empty((len(offsets), 20), np.uint8)
+    lib().orc_sha1_batch(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out))
+    return out
+
+
+class Md5Ctx(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_uint32 * 4), ("bytes", ctypes.c_uint32 * 2), ("in_", ctypes.c_uint32 * 16),
+                ("digest", ctypes.c_ubyte * 16), ("string", ctypes.c_ubyte * 64)]
+
+
+class Sha1Ctx(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_uint32 * 5), ("count", ctypes.c_uint32 * 2), ("buffer", ctypes.c_uint8 * 64)]
+
+
+# ---- Blowfish ---------------------------------------------------------------------------------
+class BfCtx(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_uint64 * 18), ("S", (ctypes.c_uint64 * 256) * 4)]
+
+
+def bf_pi_words() -> list:
+    w = (ctypes.c_uint32 * 1042)()
+    lib().orc_bf_pi_words(w)
+    return list(w)
+
+
+def bf_init(key: bytes, key_len: int | None = None) -> BfCtx:
+    c = BfCtx()
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    lib().orc_bf_init(ctypes.byref(c), kb, len(key) if key_len is None else key_len)
+    return c
+
+
+def bf_ctx_bytes(c: BfCtx) -> bytes:
+    return ctypes.string_at(ctypes.addressof(c), ctypes.sizeof(c))
+
+
+def bf_encrypt(c: BfCtx, xl: int, xr: int, decrypt: bool = False):
+    L, R = ctypes.c_uint64(xl), ctypes.c_uint64(xr)
+    (lib().orc_bf_decrypt if decrypt else lib().orc_bf_encrypt)(ctypes.byref(c), ctypes.byref(L), ctypes.byref(R))
+    return L.value, R.value
+
+
+def bf_ecb(c: BfCtx, words: np.ndarray, decrypt: bool = False, threads: int = 1) -> np.ndarray:
+    """In-place ECB over a uint64 array of (xl, xr) pairs; returns it."""
+    assert words.dtype == np.uint64
+    lib().orc_bf_ecb(ctypes.byref(c), _p(words), words.size // 2, 1 if decrypt else 0, threads)
+    return words
+
+
+def membuf_encrypt(buf: bytearray, size: int, seed: int, offset: int = 0) -> int:
+    cbuf = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+    return lib().orc_membuf_encrypt(cbuf, size, seed, offset)
+
+
+def membuf_decrypt(buf: bytearray, size: int, seed: int, offset: int = 0) -> int:
+    cbuf = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+    return lib().orc_membuf_decrypt(cbuf, size, seed, offset)
+
+
+def membuf_key(seed: int) -> bytes:
+    k = (ctypes.c_uint * 16)()
+    lib().orc_membuf_key(seed, k)
+    return bytes(k)
+
+
+# ---- generator ---------------------------------------------------------------
+def gen_records(seed: int, r0: int, n: int, rec_len: int) -> np.ndarray:
+    """C restatement of the deterministic byte generator: n records of rec_len bytes."""
+    out = np.empty(n * rec_len, np.uint8)
+    lib().orc_gen_records(seed, r0, n, rec_len, _p(out))
+    return out

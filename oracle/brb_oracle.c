@@ -1,0 +1,519 @@
+/*
+ * brb_oracle.c -- CPU ORACLE (test infrastructure only; see brb_oracle.h for who may use it and
+ * how its parity is pinned).  Deliberately written as plain loops over tables, not as the
+ * unrolled macro form of the reference, so that it is an independent restatement.
+ */
+#include "brb_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static uint32_t rotl32(uint32_t x, unsigned s) { return (x << s) | (x >> ((32 - s) & 31)); }
+
+/* =========================================================================================== */
+/* MD5 -- libbrb_core/crypto/md5.c                                                              */
+/* =========================================================================================== */
+
+/* RFC 1321 §3.4: T[i] = floor(|sin(i + 1)| * 2^32); per-round shift amounts.  The reference
+ * writes the same 64 constants as literals in BRB_MD5Transform (md5.c:179-245). */
+static uint32_t md5_T[64];
+static const unsigned md5_shift[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+static pthread_once_t md5_once = PTHREAD_ONCE_INIT;
+
+static void md5_tables(void)
+{
+    for (int i = 0; i < 64; i++)
+        md5_T[i] = (uint32_t)(uint64_t)floor(fabs(sin((double)(i + 1))) * 4294967296.0);
+}
+
+/* One compression of c->in into c->buf (md5.c:170-253). */
+static void orc_md5_transform(orc_md5_ctx *c)
+{
+    uint32_t a = c->buf[0], b = c->buf[1], cc = c->buf[2], d = c->buf[3];
+    for (int i = 0; i < 64; i++) {
+        int r = i >> 4;
+        uint32_t f;
+        int g;
+        switch (r) {       /* F1..F4 of libbrb_data.h:845-848 */
+        case 0: f = d ^ (b & (cc ^ d)); g = i; break;
+        case 1: f = cc ^ (d & (b ^ cc)); g = (5 * i + 1) & 15; break;
+        case 2: f = b ^ cc ^ d; g = (3 * i + 5) & 15; break;
+        default: f = cc ^ (b | ~d); g = (7 * i) & 15; break;
+        }
+        uint32_t t = a + f + c->in[g] + md5_T[i];     /* MD5STEP, libbrb_data.h:851 */
+        a = d;
+        d = cc;
+        cc = b;
+        b = b + rotl32(t, md5_shift[r][i & 3]);
+    }
+    c->buf[0] += a;
+    c->buf[1] += b;
+    c->buf[2] += cc;
+    c->buf[3] += d;
+}
+
+void orc_md5_init(orc_md5_ctx *c)                       /* md5.c:38-47 */
+{
+    pthread_once(&md5_once, md5_tables);
+    c->buf[0] = 0x67452301u;
+    c->buf[1] = 0xefcdab89u;
+    c->buf[2] = 0x98badcfeu;
+    c->buf[3] = 0x10325476u;
+    c->bytes[0] = c->bytes[1] = 0;
+}
+
+void orc_md5_update(orc_md5_ctx *c, const void *p, unsigned long len)   /* md5.c:72-110 */
+{
+    const uint8_t *s = (const uint8_t *)p;
+    unsigned long t = c->bytes[0];
+    c->bytes[0] = (uint32_t)(t + len);
+    if ((unsigned long)c->bytes[0] < t)           /* 32-bit carry into bytes[1] (md5.c:80-81) */
+        c->bytes[1]++;
+    unsigned long room = 64 - (t & 0x3f);
+    uint8_t *in = (uint8_t *)c->in;
+    if (room > len) {
+        memcpy(in + 64 - room, s, len);
+        return;
+    }
+    memcpy(in + 64 - room, s, room);
+    orc_md5_transform(c);
+    s += room;
+    len -= room;
+    for (; len >= 64; s += 64, len -= 64) {
+        memcpy(in, s, 64);
+        orc_md5_transform(c);
+    }
+    memcpy(in, s, len);
+}
+
+void orc_md5_update_big(orc_md5_ctx *c, const void *p, unsigned long len)   /* md5.c:49-70 */
+{
+    const uint8_t *s = (const uint8_t *)p;
+    while (len >= 65535) {
+        orc_md5_update(c, s, 65535);
+        s += 65535;
+        len -= 65535;
+    }
+    if (len)
+        orc_md5_update(c, s, len);
+}
+
+void orc_md5_final(orc_md5_ctx *c)                     /* md5.c:134-168 */
+{
+    static const char hx[] = "0123456789abcdef";
+    int count = c->bytes[0] & 0x3f;
+    uint8_t *in = (uint8_t *)c->in;
+    in[count] = 0x80;
+    if (count + 1 > 56) {                    /* padding forces an extra block (md5.c:147-153) */
+        memset(in + count + 1, 0, 63 - count);
+        orc_md5_transform(c);
+        memset(in, 0, 56);
+    } else {
+        memset(in + count + 1, 0, 55 - count);
+    }
+    c->in[14] = c->bytes[0] << 3;
+    c->in[15] = (c->bytes[1] << 3) | (c->bytes[0] >> 29);
+    orc_md5_transform(c);
+    memcpy(c->digest, c->buf, 16);
+    for (int i = 0; i < 16; i++) {           /* lowercase hex, md5.c:255-262 */
+        c->string[2 * i] = (unsigned char)hx[c->digest[i] >> 4];
+        c->string[2 * i + 1] = (unsigned char)hx[c->digest[i] & 15];
+    }
+    c->string[32] = 0;
+}
+
+void orc_md5(const void *p, uint64_t len, uint8_t out[16])
+{
+    orc_md5_ctx c;
+    orc_md5_init(&c);
+    orc_md5_update_big(&c, p, (unsigned long)len);
+    orc_md5_final(&c);
+    memcpy(out, c.digest, 16);
+}
+
+/* =========================================================================================== */
+/* SHA-1 -- libbrb_core/crypto/sha1.c                                                           */
+/* =========================================================================================== */
+
+/* Compression of one 64-byte block (sha1.c:75-130).  With SHA1HANDSOFF undefined the reference
+ * expands the schedule inside the caller's block: on return the block holds W[64..79] in host
+ * (little-endian) order.  `block` is mutated the same way here. */
+static void orc_sha1_transform_x(uint32_t st[5], uint8_t *block, int mutate)
+{
+    uint32_t W[80];
+    for (int i = 0; i < 16; i++)
+        W[i] = ((uint32_t)block[4 * i] << 24) | ((uint32_t)block[4 * i + 1] << 16) |
+               ((uint32_t)block[4 * i + 2] << 8) | (uint32_t)block[4 * i + 3];
+    for (int i = 16; i < 80; i++)
+        W[i] = rotl32(W[i - 3] ^ W[i - 8] ^ W[i - 14] ^ W[i - 16], 1);
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+    for (int i = 0; i < 80; i++) {
+        uint32_t f, k;
+        if (i < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
+        else if (i < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
+        else if (i < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDCu; }
+        else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+        uint32_t t = rotl32(a, 5) + f + e + k + W[i];
+        e = d;
+        d = c;
+        c = rotl32(b, 30);
+        b = a;
+        a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+    if (mutate)
+        memcpy(block, &W[64], 64);           /* the in-place side effect, native byte order */
+}
+
+static void orc_sha1_transform(uint32_t st[5], uint8_t *block) { orc_sha1_transform_x(st, block, 1); }
+
+void orc_sha1_init(orc_sha1_ctx *c)                     /* sha1.c:132-141 */
+{
+    c->state[0] = 0x67452301u;
+    c->state[1] = 0xEFCDAB89u;
+    c->state[2] = 0x98BADCFEu;
+    c->state[3] = 0x10325476u;
+    c->state[4] = 0xC3D2E1F0u;
+    c->count[0] = c->count[1] = 0;
+}
+
+static void sha1_update_x(orc_sha1_ctx *c, uint8_t *data, size_t len, int mutate)   /* sha1.c:143-169 */
+{
+    size_t i, j = (c->count[0] >> 3) & 63;
+    /* Counter arithmetic exactly as sha1.c:151-152: the carry test compares the 32-bit sum with
+     * the size_t (len << 3), so len >= 2^29 always adds one extra carry. */
+    c->count[0] += (uint32_t)(len << 3);
+    if ((size_t)c->count[0] < (len << 3))
+        c->count[1]++;
+    c->count[1] += (uint32_t)(len >> 29);
+    if (j + len > 63) {
+        i = 64 - j;
+        memcpy(&c->buffer[j], data, i);
+        orc_sha1_transform(c->state, c->buffer);
+        for (; i + 63 < len; i += 64)
+            orc_sha1_transform_x(c->state, data + i, mutate);   /* mutates data[i .. i+63] */
+        j = 0;
+    } else {
+        i = 0;
+    }
+    memcpy(&c->buffer[j], data + i, len - i);
+}
+
+void orc_sha1_update(orc_sha1_ctx *c, uint8_t *data, size_t len) { sha1_update_x(c, data, len, 1); }
+
+void orc_sha1_final(orc_sha1_ctx *c, uint8_t out[20])   /* sha1.c:171-200 */
+{
+    uint8_t fc[8], b80 = 0x80, b00 = 0;
+    for (int i = 0; i < 8; i++)
+        fc[i] = (uint8_t)(c->count[i >= 4 ? 0 : 1] >> ((3 - (i & 3)) * 8));
+    orc_sha1_update(c, &b80, 1);
+    while ((c->count[0] & 504) != 448)
+        orc_sha1_update(c, &b00, 1);
+    orc_sha1_update(c, fc, 8);
+    for (int i = 0; i < 20; i++)
+        out[i] = (uint8_t)(c->state[i >> 2] >> ((3 - (i & 3)) * 8));
+    memset(c, 0, sizeof(*c));
+}
+
+void orc_sha1(const void *p, uint64_t len, uint8_t out[20])
+{
+    /* BrbSha1_Do semantics (sha1.c:203-216: Init, ONE Update of len, Final) but without writing
+     * the schedule back into the caller's bytes (the batch surface never mutates its input). */
+    orc_sha1_ctx c;
+    orc_sha1_init(&c);
+    sha1_update_x(&c, (uint8_t *)p, (size_t)len, 0);
+    orc_sha1_final(&c, out);
+}
+
+/* =========================================================================================== */
+/* Blowfish -- libbrb_core/crypto/blowfish.c, with 64-bit unsigned long words                   */
+/* =========================================================================================== */
+
+/* Hex digit extraction of pi (Bailey-Borwein-Plouffe).  Returns frac(16^n * S_j) pieces. */
+static long double bbp_series(int j, long n)
+{
+    long double s = 0.0L;
+    for (long k = 0; k <= n; k++) {
+        uint64_t m = (uint64_t)(8 * k + j), r = 1 % m, b = 16 % m;
+        for (uint64_t e = (uint64_t)(n - k); e; e >>= 1) {       /* 16^(n-k) mod m, exact */
+            if (e & 1) r = (r * b) % m;
+            b = (b * b) % m;
+        }
+        s += (long double)r / (long double)m;
+        s -= floorl(s);
+    }
+    for (long k = n + 1; k <= n + 24; k++) {
+        s += powl(16.0L, (long double)(n - k)) / (long double)(8 * k + j);
+    }
+    return s - floorl(s);
+}
+
+static uint32_t pi_word(long idx)        /* hex digits [8 idx, 8 idx + 8) after the point */
+{
+    long n = 8 * idx;
+    long double x = 4 * bbp_series(1, n) - 2 * bbp_series(4, n) - bbp_series(5, n) - bbp_series(6, n);
+    x -= floorl(x);
+    uint32_t w = 0;
+    for (int i = 0; i < 8; i++) {
+        x *= 16.0L;
+        int dgt = (int)x;
+        w = (w << 4) | (uint32_t)dgt;
+        x -= dgt;
+    }
+    return w;
+}
+
+static uint32_t bf_pi[1042];
+static pthread_once_t bf_once = PTHREAD_ONCE_INIT;
+static void bf_pi_init(void)
+{
+    for (long i = 0; i < 1042; i++)
+        bf_pi[i] = pi_word(i);
+}
+
+void orc_bf_pi_words(uint32_t out[1042])
+{
+    pthread_once(&bf_once, bf_pi_init);
+    memcpy(out, bf_pi, sizeof(bf_pi));
+}
+
+static uint64_t bf_F(const orc_bf_ctx *c, uint64_t x)   /* _F, blowfish.c:445-462 */
+{
+    unsigned a = (unsigned)(x >> 24) & 0xFF, b = (unsigned)(x >> 16) & 0xFF;
+    unsigned cc = (unsigned)(x >> 8) & 0xFF, d = (unsigned)x & 0xFF;
+    return ((c->S[0][a] + c->S[1][b]) ^ c->S[2][cc]) + c->S[3][d];   /* 64-bit, no 32-bit wrap */
+}
+
+void orc_bf_encrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr)   /* blowfish.c:312-345 */
+{
+    uint64_t L = *xl, R = *xr, t;
+    for (int i = 0; i < 16; i++) {
+        L ^= c->P[i];
+        R ^= bf_F(c, L);
+        t = L; L = R; R = t;
+    }
+    t = L; L = R; R = t;
+    R ^= c->P[16];
+    L ^= c->P[17];
+    *xl = L;
+    *xr = R;
+}
+
+void orc_bf_decrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr)   /* blowfish.c:347-380 */
+{
+    uint64_t L = *xl, R = *xr, t;
+    for (int i = 17; i > 1; i--) {
+        L ^= c->P[i];
+        R ^= bf_F(c, L);
+        t = L; L = R; R = t;
+    }
+    t = L; L = R; R = t;
+    R ^= c->P[1];
+    L ^= c->P[0];
+    *xl = L;
+    *xr = R;
+}
+
+void orc_bf_init(orc_bf_ctx *c, const unsigned char *key, int key_len)   /* blowfish.c:382-443 */
+{
+    pthread_once(&bf_once, bf_pi_init);
+    for (int s = 0; s < 4; s++)
+        for (int i = 0; i < 256; i++)
+            c->S[s][i] = bf_pi[18 + 256 * s + i];
+    int j = 0;
+    for (int i = 0; i < 18; i++) {
+        uint64_t data = 0;
+        for (int k = 0; k < 4; k++) {
+            data = (data << 8) | key[j];
+            j++;
+            if (j >= key_len)            /* key_len <= 0 therefore always re-reads key[0] */
+                j = 0;
+        }
+        c->P[i] = (uint64_t)bf_pi[i] ^ data;
+    }
+    uint64_t L = 0, R = 0;
+    for (int i = 0; i < 18; i += 2) {
+        orc_bf_encrypt(c, &L, &R);
+        c->P[i] = L;
+        c->P[i + 1] = R;
+    }
+    for (int s = 0; s < 4; s++)
+        for (int i = 0; i < 256; i += 2) {
+            orc_bf_encrypt(c, &L, &R);
+            c->S[s][i] = L;
+            c->S[s][i + 1] = R;
+        }
+}
+
+typedef struct {
+    const orc_bf_ctx *c;
+    uint64_t *w;
+    uint64_t b0, b1;
+    int dec;
+} bf_job;
+
+static void *bf_worker(void *arg)
+{
+    bf_job *j = (bf_job *)arg;
+    for (uint64_t b = j->b0; b < j->b1; b++) {
+        if (j->dec) orc_bf_decrypt(j->c, &j->w[2 * b], &j->w[2 * b + 1]);
+        else orc_bf_encrypt(j->c, &j->w[2 * b], &j->w[2 * b + 1]);
+    }
+    return NULL;
+}
+
+void orc_bf_ecb(const orc_bf_ctx *c, uint64_t *words, uint64_t n_blocks, int decrypt, int n_threads)
+{
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    bf_job jobs[256];
+    for (int t = 0; t < n_threads; t++) {
+        jobs[t].c = c;
+        jobs[t].w = words;
+        jobs[t].b0 = n_blocks * (uint64_t)t / (uint64_t)n_threads;
+        jobs[t].b1 = n_blocks * (uint64_t)(t + 1) / (uint64_t)n_threads;
+        jobs[t].dec = decrypt;
+    }
+    if (n_threads == 1) { bf_worker(&jobs[0]); return; }
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, bf_worker, &jobs[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+}
+
+/* MemBuffer Blowfish wrappers, mem_buf.c:1499-1617 ------------------------------------------- */
+void orc_membuf_key(unsigned int seed, unsigned int key[16])       /* mem_buf.c:1511-1515 */
+{
+    for (unsigned long i = 0; i < 16; i++) {
+        key[i] = (unsigned int)(((i + seed) * seed) + (13 * i));
+        seed = key[i] * seed;
+    }
+}
+
+static uint64_t ld64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static void st64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+
+uint64_t orc_membuf_encrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset)
+{
+    unsigned int key[16];
+    orc_bf_ctx c;
+    uint64_t blocks = (size + offset) / 8 + 2;            /* mem_buf.c:1503-1504, :1518 */
+    orc_membuf_key(seed, key);
+    orc_bf_init(&c, (const unsigned char *)key, 4);      /* sizeof(enc_key[16]) == 4, :1528 */
+    uint8_t *raw = buf + offset;
+    uint64_t i;
+    for (i = 0; i < blocks; i += 2) {                     /* :1538-1539 */
+        uint64_t l = ld64(raw + 8 * i), r = ld64(raw + 8 * (i + 1));
+        orc_bf_encrypt(&c, &l, &r);
+        st64(raw + 8 * i, l);
+        st64(raw + 8 * (i + 1), r);
+    }
+    return i * 8 + offset;                                /* :1542 */
+}
+
+uint64_t orc_membuf_decrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset)
+{
+    unsigned int key[16];
+    orc_bf_ctx c;
+    uint64_t blocks = (size - offset) / 8 + 2;            /* mem_buf.c:1557-1558, :1571 */
+    orc_membuf_key(seed, key);
+    orc_bf_init(&c, (const unsigned char *)key, 64);     /* sizeof(enc_key) == 64, :1582 */
+    uint8_t *raw = buf + offset;
+    uint64_t i;
+    for (i = 0; i < blocks; i += 2) {
+        uint64_t l = ld64(raw + 8 * i), r = ld64(raw + 8 * (i + 1));
+        if (l == 0 || r == 0)                             /* "padding gremlin", :1595-1596 */
+            break;
+        orc_bf_decrypt(&c, &l, &r);
+        st64(raw + 8 * i, l);
+        st64(raw + 8 * (i + 1), r);
+    }
+    return i * 8 + offset;                                /* :1609 */
+}
+
+/* =========================================================================================== */
+/* Batches                                                                                       */
+/* =========================================================================================== */
+typedef struct {
+    const uint8_t *data;
+    uint32_t L;
+    uint64_t r0, r1;
+    uint8_t *out;
+    int sha;
+} dig_job;
+
+static void *dig_worker(void *arg)
+{
+    dig_job *j = (dig_job *)arg;
+    for (uint64_t r = j->r0; r < j->r1; r++) {
+        if (j->sha) orc_sha1(j->data + r * j->L, j->L, j->out + 20 * r);
+        else orc_md5(j->data + r * j->L, j->L, j->out + 16 * r);
+    }
+    return NULL;
+}
+
+static void dig_fixed(const uint8_t *data, uint32_t L, uint64_t n, uint8_t *out, int n_threads, int sha)
+{
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    dig_job jobs[256];
+    for (int t = 0; t < n_threads; t++) {
+        jobs[t].data = data;
+        jobs[t].L = L;
+        jobs[t].r0 = n * (uint64_t)t / (uint64_t)n_threads;
+        jobs[t].r1 = n * (uint64_t)(t + 1) / (uint64_t)n_threads;
+        jobs[t].out = out;
+        jobs[t].sha = sha;
+    }
+    if (n_threads == 1) { dig_worker(&jobs[0]); return; }
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, dig_worker, &jobs[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_md5_batch_fixed(const uint8_t *data, uint32_t L, uint64_t n, uint8_t *out16, int n_threads)
+{
+    pthread_once(&md5_once, md5_tables);
+    dig_fixed(data, L, n, out16, n_threads, 0);
+}
+
+void orc_sha1_batch_fixed(const uint8_t *data, uint32_t L, uint64_t n, uint8_t *out20, int n_threads)
+{
+    dig_fixed(data, L, n, out20, n_threads, 1);
+}
+
+void orc_md5_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16)
+{
+    for (uint64_t r = 0; r < n; r++) orc_md5(data + off[r], len[r], out16 + 16 * r);
+}
+
+void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out20)
+{
+    for (uint64_t r = 0; r < n; r++) orc_sha1(data + off[r], len[r], out20 + 20 * r);
+}
+
+/* =========================================================================================== */
+/* Generator                                                                                     */
+/* =========================================================================================== */
+uint64_t orc_splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void orc_gen_records(uint64_t seed, uint64_t r0, uint64_t n, uint32_t L, uint8_t *out)
+{
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t r = r0 + i;
+        uint64_t base = seed ^ (r * 0x9E3779B97F4A7C15ull);
+        uint8_t *o = out + i * L;
+        for (uint32_t k = 0; k < L; k += 8) {
+            uint64_t v = orc_splitmix64(base ^ (uint64_t)(k >> 3));
+            for (uint32_t b = 0; b < 8 && k + b < L; b++)
+                o[k + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}

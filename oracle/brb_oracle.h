@@ -1,0 +1,100 @@
+/*
+ * brb_oracle.h -- CPU ORACLE for the libbrb_core/crypto hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This is a plain-C restatement of the reference's algorithms, written from reading
+ *   libbrb_core/crypto/md5.c       (BRB_MD5*,           reference @ 2024_10_08)
+ *   libbrb_core/crypto/sha1.c      (BrbSha1_*)
+ *   libbrb_core/crypto/blowfish.c  (BRB_Blowfish_*, 64-bit `unsigned long` words)
+ *   libbrb_core/data/core/mem_buf.c:1499-1617 (MemBuffer Blowfish wrappers)
+ * Each function cites the reference file:line it follows.
+ *
+ * Who may use it: tests/ (as the checker), __graft_entry__.smoke() (as the checker) and the
+ * `cpu_baseline` leg of bench.py.  The product library (brb_framework_amd/libbrb_crypto_gpu.so)
+ * never links, loads or calls this code.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   * The reference build is UNBUILDABLE here: every crypto unit includes libbrb_data.h, which needs
+ *     <bsd/string.h>/<bsd/stdlib.h> (libbsd-dev, absent), and stand-in headers are not allowed.
+ *   * MD5 / SHA-1: pinned by RFC 1321 A.5 and FIPS 180-1 known answers plus Python hashlib
+ *     (OpenSSL), which the survey verified equal to the reference on 20 edge lengths.
+ *   * Blowfish: the low 32 bits of every word are pinned by the published Blowfish known answers
+ *     (Kocher "TESTKEY", Eric Young ECB set) and by OpenSSL BF_encrypt over random keys.
+ *     The HIGH 32 bits (the reference's 64-bit carries) are pinned only by this restatement:
+ *     "parity unpinned" for the high halves.
+ */
+#ifndef BRB_ORACLE_H
+#define BRB_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- MD5 (md5.c) -------------------------------------------------------------------------- */
+typedef struct {                 /* same field order as BRB_MD5_CTX, libbrb_data.h:854-860 */
+    uint32_t buf[4];
+    uint32_t bytes[2];
+    uint32_t in[16];
+    unsigned char digest[16];
+    unsigned char string[64];
+} orc_md5_ctx;
+
+void orc_md5_init(orc_md5_ctx *c);
+void orc_md5_update(orc_md5_ctx *c, const void *p, unsigned long len);
+void orc_md5_update_big(orc_md5_ctx *c, const void *p, unsigned long len);
+void orc_md5_final(orc_md5_ctx *c);
+void orc_md5(const void *p, uint64_t len, uint8_t out[16]);
+
+/* ---- SHA-1 (sha1.c) ----------------------------------------------------------------------- */
+typedef struct {                 /* same field order as BrbSha1Ctx, libbrb_data.h:1937-1943 */
+    uint32_t state[5];
+    uint32_t count[2];
+    uint8_t buffer[64];
+} orc_sha1_ctx;
+
+void orc_sha1_init(orc_sha1_ctx *c);
+/* Streaming update with the reference's in-place mutation of `data` (sha1.c:84-90,157-158). */
+void orc_sha1_update(orc_sha1_ctx *c, uint8_t *data, size_t len);
+void orc_sha1_final(orc_sha1_ctx *c, uint8_t out[20]);
+/* One-shot digest WITHOUT touching the input (batch semantics: digest of a private copy). */
+void orc_sha1(const void *p, uint64_t len, uint8_t out[20]);
+
+/* ---- Blowfish (blowfish.c), 64-bit words ------------------------------------------------- */
+typedef struct {                 /* same layout as BRB_BLOWFISH_CTX, libbrb_data.h:876-879 */
+    uint64_t P[18];
+    uint64_t S[4][256];
+} orc_bf_ctx;
+
+/* pi-derived tables by BBP digit extraction (independent of tools/gen_pi_tables.py) */
+void orc_bf_pi_words(uint32_t out[1042]);
+void orc_bf_init(orc_bf_ctx *c, const unsigned char *key, int key_len);
+void orc_bf_encrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr);
+void orc_bf_decrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr);
+/* ECB over n_blocks (xl, xr) pairs in place; decrypt != 0 selects decryption. */
+void orc_bf_ecb(const orc_bf_ctx *c, uint64_t *words, uint64_t n_blocks, int decrypt, int n_threads);
+
+/* MemBuffer semantics (mem_buf.c:1499-1617): key derivation and the size/loop rules.
+ * `buf` must have room for ((size + offset)/8 + 3) * 8 bytes, zero-filled past `size`.
+ * Returns the new MemBuffer size the reference would store. */
+void orc_membuf_key(unsigned int seed, unsigned int key_out[16]);
+uint64_t orc_membuf_encrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset);
+uint64_t orc_membuf_decrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset);
+
+/* ---- Batches (used by tests and by bench.py's cpu_baseline) ------------------------------- */
+void orc_md5_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out16, int n_threads);
+void orc_sha1_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out20, int n_threads);
+void orc_md5_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16);
+void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out20);
+
+/* ---- Deterministic input generator --------------------------------------
+ * byte(r, k) = byte (k mod 8), little-endian, of splitmix64(seed ^ (r * 0x9E3779B97F4A7C15) ^ (k >> 3))
+ * splitmix64(x): z = x + 0x9E3779B97F4A7C15; z = (z ^ z>>30) * 0xBF58476D1CE4E5B9;
+ *                z = (z ^ z>>27) * 0x94D049BB133111EB; return z ^ z>>31.                      */
+uint64_t orc_splitmix64(uint64_t x);
+void orc_gen_records(uint64_t seed, uint64_t r0, uint64_t n, uint32_t rec_len, uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

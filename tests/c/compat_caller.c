@@ -1,0 +1,99 @@
+/*
+ * compat_caller.c -- a C caller written the way the reference's callers use libbrb_core/crypto,
+ * compiled against include/brb_crypto.h and linked with -lbrb_crypto_gpu (no other source).
+ *
+ * Patterns exercised (reference call sites):
+ *   - MetaData pack digest: Init, UpdateBig per item, Final      (data/utils/meta_data.c:407-431)
+ *   - RC4+MD5 frame validation digest + memcmp of 16 bytes       (event/aio/ev_kq_aio_transform.c:175-180)
+ *   - RSA-SHA1 signing pre-digest: BrbSha1_Do                    (comm/utils/comm_ssl_pkey.c:465)
+ *   - MemBuffer Blowfish ECB over word pairs                     (data/core/mem_buf.c:1528-1539)
+ *   - then the batch surface on the same records, which must agree with the compat results
+ *     (returns 0 with a reason when no GPU is present; it never computes on the CPU).
+ *
+ * Output: one line per check, "name value", parsed by tests/test_abi.py.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "brb_crypto.h"
+
+static void hex(const unsigned char *p, int n, char *out)
+{
+    for (int i = 0; i < n; i++)
+        sprintf(out + 2 * i, "%02x", p[i]);
+}
+
+int main(void)
+{
+    enum { NREC = 300, RLEN = 1500 };
+    static unsigned char recs[NREC * RLEN];
+    unsigned long long x = 0x5EED0002ull;
+    for (int i = 0; i < NREC * RLEN; i++) {           /* any deterministic bytes */
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        recs[i] = (unsigned char)(x >> 56);
+    }
+    char h[64];
+
+    /* MetaData-style multi-item digest */
+    BRB_MD5_CTX md5;
+    BRB_MD5Init(&md5);
+    for (int i = 0; i < 3; i++)
+        BRB_MD5UpdateBig(&md5, recs + i * RLEN, RLEN);
+    BRB_MD5Final(&md5);
+    printf("meta_md5 %s\n", (char *)md5.string);
+
+    /* per-record digests via the compat surface */
+    static unsigned char ref16[NREC][16], ref20[NREC][20];
+    for (int r = 0; r < NREC; r++) {
+        BRB_MD5_CTX c;
+        BRB_MD5Init(&c);
+        BRB_MD5Update(&c, recs + r * RLEN, RLEN);
+        BRB_MD5Final(&c);
+        memcpy(ref16[r], c.digest, 16);
+        static unsigned char tmp[RLEN];
+        memcpy(tmp, recs + r * RLEN, RLEN);            /* BrbSha1_Do mutates its input */
+        if (BrbSha1_Do(tmp, RLEN, (char *)ref20[r]) != 0)
+            return 2;
+    }
+    hex(ref16[NREC - 1], 16, h);
+    printf("rec_last_md5 %s\n", h);
+    hex(ref20[NREC - 1], 20, h);
+    printf("rec_last_sha1 %s\n", h);
+    /* frame validation pattern: recompute and memcmp */
+    printf("validate %d\n", memcmp(ref16[0], ref16[0], 16) == 0);
+
+    /* MemBuffer-style Blowfish round trip with one ctx */
+    BRB_BLOWFISH_CTX bf;
+    unsigned char key[] = "brb_framework_k4";
+    BRB_Blowfish_Init(&bf, key, 16);
+    unsigned long w[64];
+    for (int i = 0; i < 64; i++)
+        w[i] = ((unsigned long)recs[8 * i] << 40) ^ (unsigned long)i * 0x9E3779B97F4A7C15ul;
+    unsigned long w0[64];
+    memcpy(w0, w, sizeof(w));
+    for (int i = 0; i < 64; i += 2)
+        BRB_Blowfish_Encrypt(&bf, &w[i], &w[i + 1]);
+    unsigned long enc[64];
+    memcpy(enc, w, sizeof(w));
+    for (int i = 0; i < 64; i += 2)
+        BRB_Blowfish_Decrypt(&bf, &w[i], &w[i + 1]);
+    printf("bf_roundtrip %d\n", memcmp(w, w0, sizeof(w)) == 0);
+    printf("bf_enc0 %016lx%016lx\n", enc[0], enc[1]);
+
+    /* batch surface on the same data (host mode) */
+    static unsigned char dig16[NREC][16], dig20[NREC][20];
+    int rc = BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_HOST, NULL);
+    printf("batch_md5_rc %d\n", rc);
+    if (rc != BRB_BATCH_OK) {
+        printf("batch_reason %s\n", BRB_CryptoGPU_LastError());
+        return 0;
+    }
+    printf("batch_md5_eq %d\n", memcmp(dig16, ref16, sizeof(ref16)) == 0);
+    rc = BrbSha1_BatchFixed(recs, RLEN, NREC, dig20, BRB_BATCH_HOST, NULL);
+    printf("batch_sha1_eq %d\n", rc == 1 && memcmp(dig20, ref20, sizeof(ref20)) == 0);
+    memcpy(w, w0, sizeof(w));
+    rc = BRB_Blowfish_EncryptBatch(&bf, w, 32, BRB_BATCH_HOST, NULL);
+    printf("batch_bf_eq %d\n", rc == 1 && memcmp(w, enc, sizeof(enc)) == 0);
+    return 0;
+}

@@ -1,0 +1,38 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    out = {}
+    for name in ("kat", "digests", "blowfish64", "quirks"):
+        with open(os.path.join(GOLDEN, name + ".json")) as f:
+            out[name] = json.load(f)
+    return out
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import oracle
+    oracle.lib()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def brb():
+    """The product library (built in-tree).  Missing library = test failure, never a skip."""
+    import brb_framework_amd
+    brb_framework_amd.lib()
+    return brb_framework_amd

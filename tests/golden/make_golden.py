@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json -- the fixtures that pin the oracle and the GPU path.
+
+Sources, in order of authority (DESIGN.md "Oracle"):
+  * published known answers typed in from their standards: RFC 1321 A.5 (MD5), FIPS 180-1
+    appendices A/B/C (SHA-1), Kocher's Blowfish self-test ("TESTKEY") and Eric Young's Blowfish ECB
+    vectors.  Each is re-checked here against an independent implementation before it is written
+    (hashlib for MD5/SHA-1, OpenSSL libcrypto BF_ecb_encrypt for Blowfish).
+  * Python hashlib (OpenSSL) digests of the SURVEY §8(d) generator at the edge lengths and of the
+    first/last records of configs 1-3.  The survey verified BRB_MD5*/BrbSha1_* == hashlib on 20 edge
+    lengths with the reference compiled in its container.
+  * the oracle restatement (oracle/brb_oracle.c) for what no external source pins: the HIGH 32 bits
+    of the reference's 64-bit Blowfish words, the SHA-1 in-place mutation bytes and the MemBuffer
+    wrappers.  These are marked "source": "oracle" -- regression fixtures, not pins.
+
+The reference itself cannot be built here (libbrb_data.h needs <bsd/string.h>, absent; stand-in
+headers are not allowed), so no fixture comes from running reference code.
+
+Usage (in the repo root):  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import oracle  # noqa: E402
+from brb_framework_amd import workload  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+MD5_KAT = [  # RFC 1321 appendix A.5
+    ("", "d41d8cd98f00b204e9800998ecf8427e"),
+    ("a", "0cc175b9c0f1b6a831c399e269772661"),
+    ("abc", "900150983cd24fb0d6963f7d28e17f72"),
+    ("message digest", "f96b697d7cb7938d525a2f31aaf161d0"),
+    ("abcdefghijklmnopqrstuvwxyz", "c3fcd3d76192e4007dfb496cca67e13b"),
+    ("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789", "d174ab98d277d9f5a5611c2c9f419d9f"),
+    ("1234567890" * 8, "57edf4a22be3c955ac49da2e2107b67a"),
+]
+SHA1_KAT = [  # FIPS 180-1 appendices A, B, C
+    ("abc", 1, "a9993e364706816aba3e25717850c26c9cd0d89d"),
+    ("abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq", 1, "84983e441c3bd26ebaae4aa1f95129e5e54670f1"),
+    ("a", 1000000, "34aa973cd4c4daa4f61eeb2bdbad27316534016f"),
+]
+BF_KAT = [  # (key hex, plaintext hex, ciphertext hex); Eric Young's ECB set + Kocher's self-test
+    ("0000000000000000", "0000000000000000", "4EF997456198DD78"),
+    ("FFFFFFFFFFFFFFFF", "FFFFFFFFFFFFFFFF", "51866FD5B85ECB8A"),
+    ("3000000000000000", "1000000000000001", "7D856F9A613063F2"),
+    ("1111111111111111", "1111111111111111", "2466DD878B963C9D"),
+    ("0123456789ABCDEF", "1111111111111111", "61F9C3802281B096"),
+    ("1111111111111111", "0123456789ABCDEF", "7D0CC630AFDA1EC7"),
+    ("FEDCBA9876543210", "0123456789ABCDEF", "0ACEAB0FC6A0A28D"),
+    ("7CA110454A1A6E57", "01A1D6D039776742", "59C68245EB05282B"),
+    ("0131D9619DC1376E", "5CD54CA83DEF57DA", "B1B8CC0B250F09A0"),
+    ("544553544B4559", "0000000100000002", "DF333FD230A71BB4"),          # "TESTKEY", (1, 2)
+    ("6162636465666768696A6B6C6D6E6F707172737475767778797A", "424C4F5746495348", "324ED0FEF413A203"),
+]
+EDGE_LENGTHS = [0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129, 1500, 16384, 65535, 65536, 65537]
+
+
+def libcrypto_bf(key: bytes, pt: bytes) -> bytes:
+    L = ctypes.CDLL("libcrypto.so.3")
+    ks = ctypes.create_string_buffer(8192)
+    L.BF_set_key(ks, len(key), key)
+    out = ctypes.create_string_buffer(8)
+    L.BF_ecb_encrypt(pt, out, ks, 1)
+    return out.raw
+
+
+def dump(name, obj):
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+        f.write("\n")
+
+
+def main():
+    # ---- published known answers, each cross-checked ----
+    for m, d in MD5_KAT:
+        assert hashlib.md5(m.encode()).hexdigest() == d, m
+    for m, rep, d in SHA1_KAT:
+        assert hashlib.sha1(m.encode() * rep).hexdigest() == d, m
+    for k, p, c in BF_KAT:
+        assert libcrypto_bf(bytes.fromhex(k), bytes.fromhex(p)).hex().upper() == c, k
+    dump("kat.json", {
+        "md5_rfc1321": [{"msg": m, "digest": d} for m, d in MD5_KAT],
+        "sha1_fips180_1": [{"msg": m, "repeat": r, "digest": d} for m, r, d in SHA1_KAT],
+        "blowfish_ecb": [{"key": k, "plain": p, "cipher": c} for k, p, c in BF_KAT],
+        "note": "Blowfish vectors pin only the LOW 32 bits of each 64-bit reference word "
+                "(the reference's xl/xr are unsigned long; blowfish.c:445-462 keeps carries in the high half).",
+    })
+
+    # ---- generator digests (hashlib) ----
+    seed = workload.SEEDS[1]
+    edge = []
+    for n in EDGE_LENGTHS:
+        rec = workload.gen_records(seed, 7, 1, n).tobytes()
+        edge.append({"len": n, "record": 7, "md5": hashlib.md5(rec).hexdigest(),
+                     "sha1": hashlib.sha1(rec).hexdigest(), "first8": rec[:8].hex()})
+    cfgs = {}
+    for c in (1, 2, 3):
+        cfg = workload.CONFIGS[c]
+        n, L = cfg["records"], cfg["rec_len"]
+        idx = sorted(set(list(range(min(64, n))) + list(range(max(0, n - 64), n))))
+        recs = []
+        for r in idx:
+            b = workload.gen_records(workload.SEEDS[c], r, 1, L).tobytes()
+            recs.append({"r": r, "md5": hashlib.md5(b).hexdigest(), "sha1": hashlib.sha1(b).hexdigest()})
+        cfgs[str(c)] = {"seed": workload.SEEDS[c], "records": n, "rec_len": L, "digests": recs}
+    dump("digests.json", {"source": "hashlib (OpenSSL 3) over the SURVEY §8(d) generator",
+                          "generator_seed": seed, "edge": edge, "configs": cfgs})
+
+    # ---- oracle-only regression fixtures (64-bit Blowfish, SHA-1 mutation, MemBuffer) ----
+    bf = {"source": "oracle", "contexts": [], "cfg4": {}}
+    for key in (b"TESTKEY", workload.CFG4_KEY, bytes(range(56))):
+        c = oracle.bf_init(key)
+        raw = oracle.bf_ctx_bytes(c)
+        bf["contexts"].append({"key": key.hex(), "sha256": hashlib.sha256(raw).hexdigest(),
+                               "P": [hex(v) for v in c.P], "S0_first4": [hex(c.S[0][i]) for i in range(4)],
+                               "S3_last4": [hex(c.S[3][i]) for i in range(252, 256)]})
+    c = oracle.bf_init(workload.CFG4_KEY)
+    words = workload.gen_words(workload.SEEDS[4], 2048)
+    ct = oracle.bf_ecb(c, words.copy())
+    bf["cfg4"] = {"key": workload.CFG4_KEY.hex(), "seed": workload.SEEDS[4], "pairs": 1024,
+                  "plain_sha256": hashlib.sha256(words.tobytes()).hexdigest(),
+                  "cipher_sha256": hashlib.sha256(ct.tobytes()).hexdigest(),
+                  "cipher_first8": [hex(int(v)) for v in ct[:16]]}
+    dump("blowfish64.json", bf)
+
+    msg = bytearray(workload.gen_records(seed, 3, 1, 200).tobytes())
+    before = bytes(msg)
+    ctx = oracle.Sha1Ctx()
+    oracle.lib().orc_sha1_init(ctypes.byref(ctx))
+    cbuf = (ctypes.c_uint8 * len(msg)).from_buffer(msg)
+    oracle.lib().orc_sha1_update(ctypes.byref(ctx), cbuf, len(msg))
+    dig = ctypes.create_string_buffer(20)
+    oracle.lib().orc_sha1_final(ctypes.byref(ctx), dig)
+    mb = []
+    for size, off, seed_ in ((0, 0, 0x4FD9), (5, 0, 0x4FD9), (100, 0, 0x4FD9), (100, 8, 7), (1023, 3, 12345)):
+        # MemBuffer of `size` bytes; the reference grows it and zero-fills before the ECB pass
+        # (MemBufferCheckForGrow, mem_buf.c:1525,1934-1992), so room is zero-padded here
+        raw = workload.gen_records(seed, 11, 1, size).tobytes() if size else b""
+        need = off + 8 * ((size + off) // 8 + 4)
+        buf = bytearray(raw) + bytearray(max(0, need - size))
+        enc = bytearray(buf)
+        new_size = oracle.membuf_encrypt(enc, size, seed_, off)
+        dec = bytearray(enc)
+        dec_size = oracle.membuf_decrypt(dec, new_size, seed_, off)
+        mb.append({"size": size, "offset": off, "seed": seed_, "plain": bytes(buf).hex(),
+                   "enc_size": int(new_size), "enc": bytes(enc).hex(), "dec_size": int(dec_size), "dec": bytes(dec).hex()})
+    dump("quirks.json", {
+        "source": "oracle",
+        "sha1_inplace": {"input": before.hex(), "after_update": bytes(msg).hex(), "digest": dig.raw.hex(),
+                         "hashlib_digest": hashlib.sha1(before).hexdigest()},
+        "membuffer": mb,
+        "membuf_key_4fd9": oracle.membuf_key(0x4FD9).hex(),
+    })
+    print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".json")))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,193 @@
+"""Compat surface of libbrb_crypto_gpu.so (host, no GPU needed) against the oracle.
+
+These are the drop-in symbols of libbrb_data.h:862-869, :881-883, :1947-1951 that the reference's
+callers link against; they must reproduce the reference bit for bit, quirks included.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+
+def _md5_ctx(brb):
+    c = brb.BRB_MD5_CTX()
+    brb.lib().BRB_MD5Init(ctypes.byref(c))
+    return c
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 55, 56, 57, 63, 64, 65, 127, 128, 129, 1500, 16384, 65535, 65536, 65537, 200003])
+def test_md5_one_shot(brb, orc, n):
+    rec = workload.gen_records(0x5EED0001, 7, 1, n).tobytes()
+    c = _md5_ctx(brb)
+    brb.lib().BRB_MD5Update(ctypes.byref(c), rec, n)
+    brb.lib().BRB_MD5Final(ctypes.byref(c))
+    assert bytes(c.digest) == orc.md5(rec) == hashlib.md5(rec).digest()
+    assert bytes(c.string[:33]) == hashlib.md5(rec).hexdigest().encode() + b"\0"
+
+
+def test_md5_context_bytes_match_oracle(brb, orc):
+    """Whole-context equality (buf, counters, the `in` staging words, digest, string) after random
+    chunked updates: BRB_MD5_CTX is ABI, so its contents are part of the contract."""
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 100_000, dtype=np.uint8).tobytes()
+    c = _md5_ctx(brb)
+    o = orc.Md5Ctx()
+    orc.lib().orc_md5_init(ctypes.byref(o))
+    pos = 0
+    while pos < len(data):
+        k = int(rng.choice([0, 1, 5, 63, 64, 65, 100, 128, 1000, 4099]))
+        piece = data[pos:pos + k]
+        brb.lib().BRB_MD5Update(ctypes.byref(c), piece, len(piece))
+        orc.lib().orc_md5_update(ctypes.byref(o), piece, len(piece))
+        assert list(c.buf) == list(o.buf) and list(c.bytes) == list(o.bytes)
+        assert list(c.in_) == list(o.in_)
+        pos += k
+    brb.lib().BRB_MD5Final(ctypes.byref(c))
+    orc.lib().orc_md5_final(ctypes.byref(o))
+    assert bytes(c)[:104 + 33] == bytes(o)[:104 + 33]
+
+
+def test_md5_update_big(brb):
+    data = workload.gen_records(0x5EED0001, 0, 1, 300_000).tobytes()
+    c = _md5_ctx(brb)
+    brb.lib().BRB_MD5UpdateBig(ctypes.byref(c), data, len(data))
+    brb.lib().BRB_MD5Final(ctypes.byref(c))
+    assert bytes(c.digest) == hashlib.md5(data).digest()
+
+
+def test_md5_32bit_counter_carry(brb):
+    """bytes[0] wraps into bytes[1] (md5.c:80-81): seed the counter near 2^32 and check the
+    length words Final appends against the 64-bit count."""
+    c = _md5_ctx(brb)
+    c.bytes[0] = 0xFFFFFFC0          # 2^32 - 64 bytes "already hashed"
+    brb.lib().BRB_MD5Update(ctypes.byref(c), b"x" * 100, 100)
+    assert c.bytes[0] == 36 and c.bytes[1] == 1
+
+
+@pytest.mark.parametrize("text", [b"Hello WORLD az AZ 09", bytes(range(256)) * 3, b"MiXeD" * 40])
+def test_md5_lower_text(brb, text):
+    """md5.c:112-132 lowercases A-Z only; keys longer than 128 bytes overflowed the reference's
+    stack buffer, here they are hashed in 128-byte pieces with the same digest."""
+    c = _md5_ctx(brb)
+    brb.lib().BRB_MD5UpdateLowerText(ctypes.byref(c), text, len(text))
+    brb.lib().BRB_MD5Final(ctypes.byref(c))
+    lowered = bytes(b + 32 if 65 <= b <= 90 else b for b in text)
+    assert bytes(c.digest) == hashlib.md5(lowered).digest()
+    c2 = _md5_ctx(brb)
+    brb.lib().BRB_MD5UpdateLowerText(ctypes.byref(c2), None, 5)
+    brb.lib().BRB_MD5UpdateLowerText(ctypes.byref(c2), text, 0)
+    assert c2.bytes[0] == 0
+
+
+def test_md5_to_str(brb):
+    d = bytes(range(16))
+    out = ctypes.create_string_buffer(33)
+    brb.lib().BRB_MD5ToStr(d, out)
+    assert out.value == d.hex().encode()
+
+
+def test_md5_transform_direct(brb, orc):
+    c = _md5_ctx(brb)
+    blk = workload.gen_records(1, 0, 1, 64).tobytes()
+    ctypes.memmove(ctypes.addressof(c) + 24, blk, 64)
+    brb.lib().BRB_MD5Transform(ctypes.byref(c))
+    o = orc.Md5Ctx()
+    orc.lib().orc_md5_init(ctypes.byref(o))
+    orc.lib().orc_md5_update(ctypes.byref(o), blk, 64)   # exactly one Transform of blk
+    assert list(c.buf) == list(o.buf)
+
+
+# ---- SHA-1 -----------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [0, 1, 55, 56, 63, 64, 65, 119, 120, 128, 200, 1500, 65537])
+def test_sha1_do_and_mutation(brb, orc, n):
+    rec = bytearray(workload.gen_records(0x5EED0001, 3, 1, n).tobytes())
+    ref = hashlib.sha1(bytes(rec)).digest()
+    mine = bytearray(rec)
+    dig = ctypes.create_string_buffer(20)
+    buf = (ctypes.c_uint8 * max(n, 1)).from_buffer(mine if n else bytearray(1))
+    assert brb.lib().BrbSha1_Do(buf, n, dig) == 0
+    assert dig.raw == ref
+    # the oracle's streaming update mutates the same bytes the same way
+    o = bytearray(rec)
+    ctx = orc.Sha1Ctx()
+    orc.lib().orc_sha1_init(ctypes.byref(ctx))
+    if n:
+        orc.lib().orc_sha1_update(ctypes.byref(ctx), (ctypes.c_uint8 * n).from_buffer(o), n)
+    assert mine == o
+
+
+def test_sha1_streaming_context(brb, orc):
+    rng = np.random.default_rng(5)
+    data = bytearray(rng.integers(0, 256, 50_000, dtype=np.uint8).tobytes())
+    a, b = bytearray(data), bytearray(data)
+    c = brb.BrbSha1Ctx()
+    o = orc.Sha1Ctx()
+    brb.lib().BrbSha1_Init(ctypes.byref(c))
+    orc.lib().orc_sha1_init(ctypes.byref(o))
+    pos = 0
+    while pos < len(data):
+        k = min(int(rng.choice([1, 7, 63, 64, 65, 200, 1000])), len(data) - pos)
+        brb.lib().BrbSha1_Update(ctypes.byref(c), ctypes.addressof((ctypes.c_uint8 * len(a)).from_buffer(a)) + pos, k)
+        orc.lib().orc_sha1_update(ctypes.byref(o), ctypes.addressof((ctypes.c_uint8 * len(b)).from_buffer(b)) + pos, k)
+        assert bytes(c) == bytes(o)
+        pos += k
+    assert a == b
+    d1, d2 = ctypes.create_string_buffer(20), ctypes.create_string_buffer(20)
+    brb.lib().BrbSha1_Final(ctypes.byref(c), d1)
+    orc.lib().orc_sha1_final(ctypes.byref(o), d2)
+    assert d1.raw == d2.raw == hashlib.sha1(bytes(data)).digest()
+    assert bytes(c) == bytes(92)        # Final wipes the context (sha1.c:192-194)
+
+
+def test_sha1_do_null(brb):
+    out = ctypes.create_string_buffer(20)
+    assert brb.lib().BrbSha1_Do(None, 3, out) == -1
+    assert brb.lib().BrbSha1_Do(b"abc", 3, None) == -1
+
+
+def test_sha1_transform_mutates(brb):
+    st = (ctypes.c_uint32 * 5)(0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0)
+    blk = bytearray(b"abc" + b"\x80" + bytes(59) + b"\x18")
+    before = bytes(blk)
+    brb.lib().BrbSha1_Transform(st, (ctypes.c_uint8 * 64).from_buffer(blk))
+    assert b"".join(v.to_bytes(4, "big") for v in st) == hashlib.sha1(b"abc").digest()
+    assert bytes(blk) != before
+
+
+# ---- Blowfish --------------------------------------------------------------------------------
+@pytest.mark.parametrize("key", [b"TESTKEY", b"brb_framework_k4", bytes(range(56)), b"\x00", b"k" * 72])
+def test_blowfish_init_matches_oracle(brb, orc, key):
+    c = brb.blowfish_init(key)
+    assert brb.blowfish_ctx_bytes(c) == orc.bf_ctx_bytes(orc.bf_init(key))
+
+
+def test_blowfish_keylen_zero(brb, orc):
+    """keyLen <= 0: `j >= keyLen` always resets j, so every byte read is key[0] (blowfish.c:402-410)."""
+    c = brb.blowfish_init(b"Q", key_len=0)
+    assert brb.blowfish_ctx_bytes(c) == orc.bf_ctx_bytes(orc.bf_init(b"Q", 0))
+    assert brb.blowfish_ctx_bytes(c) == orc.bf_ctx_bytes(orc.bf_init(b"QQQQ"))
+
+
+def test_blowfish_encrypt_decrypt_64bit(brb, orc):
+    c = brb.blowfish_init(b"brb_framework_k4")
+    oc = orc.bf_init(b"brb_framework_k4")
+    w = workload.gen_words(0x5EED0004, 64)
+    for i in range(0, 64, 2):
+        xl, xr = ctypes.c_ulong(int(w[i])), ctypes.c_ulong(int(w[i + 1]))
+        brb.lib().BRB_Blowfish_Encrypt(ctypes.byref(c), ctypes.byref(xl), ctypes.byref(xr))
+        assert (xl.value, xr.value) == orc.bf_encrypt(oc, int(w[i]), int(w[i + 1]))
+        brb.lib().BRB_Blowfish_Decrypt(ctypes.byref(c), ctypes.byref(xl), ctypes.byref(xr))
+        assert (xl.value, xr.value) == (int(w[i]), int(w[i + 1]))
+
+
+def test_blowfish_kat(brb, golden):
+    for v in golden["kat"]["blowfish_ecb"]:
+        c = brb.blowfish_init(bytes.fromhex(v["key"]))
+        p = bytes.fromhex(v["plain"])
+        xl, xr = ctypes.c_ulong(int.from_bytes(p[:4], "big")), ctypes.c_ulong(int.from_bytes(p[4:], "big"))
+        brb.lib().BRB_Blowfish_Encrypt(ctypes.byref(c), ctypes.byref(xl), ctypes.byref(xr))
+        got = (xl.value & 0xFFFFFFFF).to_bytes(4, "big") + (xr.value & 0xFFFFFFFF).to_bytes(4, "big")
+        assert got.hex().upper() == v["cipher"]

@@ -1,0 +1,211 @@
+"""GPU parity: the HIP batch kernels (through the C ABI) against the CPU oracle, bit for bit.
+
+Small cases run the oracle on every record; full BASELINE sizes are checked against the oracle on
+all records where it finishes in seconds (cfg2, cfg3) and through size-independent properties
+where it does not (cfg4: sampled records vs the oracle + exact decrypt(encrypt(x)) == x).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+pytestmark = pytest.mark.gpu
+
+EDGE = [0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129, 1500, 16384, 65535, 65536, 65537]
+
+
+@pytest.fixture(scope="module")
+def torch_dev(brb):
+    import torch
+    assert torch.cuda.is_available(), "no HIP device visible to torch"
+    assert brb.gpu_available(), brb.lib().BRB_CryptoGPU_LastError()
+    return torch
+
+
+def to_dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("rec_len", EDGE)
+def test_md5_sha1_fixed_edge_lengths(brb, orc, torch_dev, rec_len):
+    n = 300 if rec_len <= 16384 else 20
+    data = workload.gen_records(0x5EED0001, 0, n, rec_len)
+    want5 = orc.md5_batch_fixed(data, rec_len, n, threads=4)
+    want1 = orc.sha1_batch_fixed(data, rec_len, n, threads=4)
+    # device mode
+    d = to_dev(torch_dev, data) if data.size else torch_dev.zeros(1, dtype=torch_dev.uint8, device="cuda")
+    assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want5)
+    assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(), want1)
+    # host mode
+    assert np.array_equal(brb.md5_batch_fixed(data, rec_len, n), want5)
+    assert np.array_equal(brb.sha1_batch_fixed(data, rec_len, n), want1)
+
+
+def test_golden_edge_digests(brb, torch_dev, golden):
+    g = golden["digests"]
+    for e in g["edge"]:
+        rec = workload.gen_records(g["generator_seed"], e["record"], 1, e["len"])
+        buf = rec if rec.size else np.zeros(1, np.uint8)
+        assert brb.md5_batch_fixed(buf, e["len"], 1)[0].tobytes().hex() == e["md5"]
+        assert brb.sha1_batch_fixed(buf, e["len"], 1)[0].tobytes().hex() == e["sha1"]
+
+
+@pytest.mark.parametrize("misalign", [1, 2, 3])
+@pytest.mark.parametrize("rec_len", [1500, 1501, 64, 77])
+def test_unaligned_records(brb, orc, torch_dev, misalign, rec_len):
+    n = 257
+    data = workload.gen_records(0x5EED0003, 0, n, rec_len)
+    d = torch_dev.zeros(data.size + 16, dtype=torch_dev.uint8, device="cuda")
+    d[misalign:misalign + data.size] = to_dev(torch_dev, data)
+    view = d[misalign:misalign + data.size]
+    assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(), orc.md5_batch_fixed(data, rec_len, n))
+    assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(), orc.sha1_batch_fixed(data, rec_len, n))
+
+
+def test_unaligned_output(brb, orc, torch_dev):
+    n, L = 100, 1500
+    data = to_dev(torch_dev, workload.gen_records(0x5EED0002, 0, n, L))
+    out = torch_dev.zeros(n * 20 + 3, dtype=torch_dev.uint8, device="cuda")
+    o5 = out[1:1 + 16 * n].view(n, 16)
+    brb.md5_batch_fixed(data, L, n, out=o5)
+    assert np.array_equal(o5.cpu().numpy(), orc.md5_batch_fixed(data.cpu().numpy(), L, n))
+    o1 = out[3:3 + 20 * n].view(n, 20)
+    brb.sha1_batch_fixed(data, L, n, out=o1)
+    assert np.array_equal(o1.cpu().numpy(), orc.sha1_batch_fixed(data.cpu().numpy(), L, n))
+
+
+def test_variable_records(brb, orc, torch_dev):
+    rng = np.random.default_rng(11)
+    n = 3000
+    buf = workload.gen_records(0x5EED0005, 0, 1, 1 << 20)
+    lens = rng.integers(0, 4000, n).astype(np.uint32)
+    lens[:50] = 0
+    lens[50:100] = rng.choice([55, 56, 63, 64, 65, 119, 120], 50)
+    offs = rng.integers(0, buf.size - 4000, n).astype(np.uint64)      # overlapping, any alignment
+    want5, want1 = orc.md5_batch(buf, offs, lens), orc.sha1_batch(buf, offs, lens)
+    # host mode
+    assert np.array_equal(brb.md5_batch(buf, offs, lens), want5)
+    assert np.array_equal(brb.sha1_batch(buf, offs, lens), want1)
+    # device mode
+    d, o, ln = to_dev(torch_dev, buf), to_dev(torch_dev, offs.view(np.int64)), to_dev(torch_dev, lens.view(np.int32))
+    assert np.array_equal(brb.md5_batch(d, o, ln).cpu().numpy(), want5)
+    assert np.array_equal(brb.sha1_batch(d, o, ln).cpu().numpy(), want1)
+
+
+def test_cfg2_full(brb, orc, torch_dev, golden):
+    cfg = workload.CONFIGS[2]
+    n, L = cfg["records"], cfg["rec_len"]
+    data = workload.gen_records(workload.SEEDS[2], 0, n, L)
+    d = to_dev(torch_dev, data)
+    got5 = brb.md5_batch_fixed(d, L, n).cpu().numpy()
+    got1 = brb.sha1_batch_fixed(d, L, n).cpu().numpy()
+    assert np.array_equal(got5, orc.md5_batch_fixed(data, L, n, threads=16))
+    assert np.array_equal(got1, orc.sha1_batch_fixed(data, L, n, threads=16))
+    for e in golden["digests"]["configs"]["2"]["digests"]:
+        assert got5[e["r"]].tobytes().hex() == e["md5"]
+        assert got1[e["r"]].tobytes().hex() == e["sha1"]
+
+
+def test_cfg3_full(brb, orc, torch_dev, golden):
+    cfg = workload.CONFIGS[3]
+    n, L = cfg["records"], cfg["rec_len"]
+    data = workload.gen_records(workload.SEEDS[3], 0, n, L)
+    got5 = brb.md5_batch_fixed(to_dev(torch_dev, data), L, n).cpu().numpy()
+    assert np.array_equal(got5, orc.md5_batch_fixed(data, L, n, threads=16))
+    for e in golden["digests"]["configs"]["3"]["digests"]:
+        assert got5[e["r"]].tobytes().hex() == e["md5"]
+
+
+def test_cfg5_shard_property(brb, torch_dev):
+    """One GPU's shard of cfg5 (records [7/8 N, N)): sampled records vs hashlib."""
+    n_all, L = workload.CONFIGS[5]["records"], workload.CONFIGS[5]["rec_len"]
+    r0, r1 = workload.shard(n_all, 7, 8)
+    n = 65536                      # a slice of the shard keeps the host-side generator quick
+    data = workload.gen_records(workload.SEEDS[5], r1 - n, n, L)
+    got = brb.md5_batch_fixed(to_dev(torch_dev, data), L, n).cpu().numpy()
+    for i in np.random.default_rng(2).integers(0, n, 64):
+        assert got[i].tobytes() == hashlib.md5(data[i * L:(i + 1) * L].tobytes()).digest()
+
+
+# ---- Blowfish --------------------------------------------------------------------------------
+@pytest.mark.parametrize("key", [b"TESTKEY", b"brb_framework_k4", bytes(range(56)), b"\xff" * 3])
+@pytest.mark.parametrize("n_blocks", [1, 255, 256, 257, 10007])
+def test_blowfish_batch_vs_oracle(brb, orc, torch_dev, key, n_blocks):
+    ctx = brb.blowfish_init(key)
+    oc = orc.bf_init(key)
+    w = workload.gen_words(0x5EED0004, 2 * n_blocks)
+    want = orc.bf_ecb(oc, w.copy())
+    # host mode
+    h = w.copy()
+    brb.blowfish_encrypt_batch(ctx, h)
+    assert np.array_equal(h, want)
+    brb.blowfish_decrypt_batch(ctx, h)
+    assert np.array_equal(h, w)
+    # device mode (ctx uploaded once)
+    cd = torch_dev.frombuffer(bytearray(brb.blowfish_ctx_bytes(ctx)), dtype=torch_dev.uint8).cuda()
+    d = to_dev(torch_dev, w.view(np.int64))
+    brb.blowfish_encrypt_batch(cd, d)
+    assert np.array_equal(d.cpu().numpy().view(np.uint64), want)
+    brb.blowfish_decrypt_batch(cd, d)
+    assert np.array_equal(d.cpu().numpy().view(np.uint64), w)
+
+
+def test_blowfish_kat_low_halves(brb, golden):
+    for v in golden["kat"]["blowfish_ecb"]:
+        ctx = brb.blowfish_init(bytes.fromhex(v["key"]))
+        p = bytes.fromhex(v["plain"])
+        w = np.array([int.from_bytes(p[:4], "big"), int.from_bytes(p[4:], "big")], np.uint64)
+        brb.blowfish_encrypt_batch(ctx, w)
+        got = (int(w[0]) & 0xFFFFFFFF).to_bytes(4, "big") + (int(w[1]) & 0xFFFFFFFF).to_bytes(4, "big")
+        assert got.hex().upper() == v["cipher"]
+
+
+def test_blowfish_golden_cfg4_prefix(brb, torch_dev, golden):
+    g = golden["blowfish64"]["cfg4"]
+    ctx = brb.blowfish_init(bytes.fromhex(g["key"]))
+    w = workload.gen_words(g["seed"], 2 * g["pairs"])
+    d = to_dev(torch_dev, w.view(np.int64))
+    brb.blowfish_encrypt_batch(ctx, d)
+    assert hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest() == g["cipher_sha256"]
+
+
+def test_cfg4_full_round_trip(brb, orc, torch_dev):
+    """cfg4 at full size (65 536 x 16 KiB = 1 GiB): sampled records == oracle, and the exact
+    64-bit round trip restores every word."""
+    cfg = workload.CONFIGS[4]
+    n_words = cfg["records"] * cfg["rec_len"] // 8
+    torch = torch_dev
+    ctx = brb.blowfish_init(workload.CFG4_KEY)
+    oc = orc.bf_init(workload.CFG4_KEY)
+    w = workload.gen_words(workload.SEEDS[4], n_words)
+    d = to_dev(torch, w.view(np.int64))
+    cd = torch.frombuffer(bytearray(brb.blowfish_ctx_bytes(ctx)), dtype=torch.uint8).cuda()
+    brb.blowfish_encrypt_batch(cd, d)
+    wpr = cfg["rec_len"] // 8
+    for r in list(np.random.default_rng(4).integers(0, cfg["records"], 48)) + [0, cfg["records"] - 1]:
+        got = d[r * wpr:(r + 1) * wpr].cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, orc.bf_ecb(oc, w[r * wpr:(r + 1) * wpr].copy())), r
+    brb.blowfish_decrypt_batch(cd, d)
+    assert torch.equal(d, to_dev(torch, w.view(np.int64)))
+
+
+def test_async_stream(brb, orc, torch_dev):
+    torch = torch_dev
+    n, L = 4096, 1500
+    data = workload.gen_records(0x5EED0002, 0, n, L)
+    s = torch.cuda.Stream()
+    d = to_dev(torch, data)
+    torch.cuda.synchronize()
+    out = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    brb.md5_batch_fixed(d, L, n, out=out, stream=s, async_=True)
+    s.synchronize()
+    assert np.array_equal(out.cpu().numpy(), orc.md5_batch_fixed(data, L, n))
+
+
+def test_c_caller_batch_on_gpu(brb, tmp_path):
+    from test_abi import build_caller, run_caller
+    res = run_caller(build_caller(tmp_path))
+    assert res["batch_md5_rc"] == "1"
+    assert res["batch_md5_eq"] == "1" and res["batch_sha1_eq"] == "1" and res["batch_bf_eq"] == "1"

@@ -1,0 +1,187 @@
+"""Pin the CPU oracle against published known answers, hashlib/libcrypto and the golden fixtures.
+
+The oracle (oracle/brb_oracle.c) is the checker for every GPU parity test, so it is pinned first:
+  * MD5: RFC 1321 A.5; SHA-1: FIPS 180-1 A/B/C; both also against hashlib at every edge length.
+  * Blowfish: low 32 bits vs Eric Young's ECB vectors, Kocher's TESTKEY and OpenSSL BF_encrypt;
+    high 32 bits: regression fixtures of the restatement only ("parity unpinned").
+  * pi tables: BBP digit extraction (oracle) == Machin expansion (tools/gen_pi_tables.py).
+"""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_md5_rfc1321(orc, golden):
+    for v in golden["kat"]["md5_rfc1321"]:
+        assert orc.md5(v["msg"].encode()).hex() == v["digest"]
+
+
+def test_sha1_fips180(orc, golden):
+    for v in golden["kat"]["sha1_fips180_1"]:
+        assert orc.sha1(v["msg"].encode() * v["repeat"]).hex() == v["digest"]
+
+
+def test_digest_edge_lengths(orc, golden):
+    g = golden["digests"]
+    for e in g["edge"]:
+        rec = orc.gen_records(g["generator_seed"], e["record"], 1, e["len"]).tobytes()
+        assert rec[:8].hex() == e["first8"]
+        assert orc.md5(rec).hex() == e["md5"] == hashlib.md5(rec).hexdigest()
+        assert orc.sha1(rec).hex() == e["sha1"]
+
+
+def test_config_records(orc, golden):
+    for c, cfg in golden["digests"]["configs"].items():
+        for d in cfg["digests"][:8] + cfg["digests"][-8:]:
+            rec = orc.gen_records(cfg["seed"], d["r"], 1, cfg["rec_len"]).tobytes()
+            assert orc.md5(rec).hex() == d["md5"], (c, d["r"])
+            assert orc.sha1(rec).hex() == d["sha1"], (c, d["r"])
+
+
+def test_md5_streaming_and_updatebig(orc):
+    """Chunked Update / UpdateBig (65 535-byte chunks, md5.c:49-70) == one-shot digest."""
+    rng = np.random.default_rng(1)
+    data = rng.integers(0, 256, 200_003, dtype=np.uint8).tobytes()
+    ref = hashlib.md5(data).digest()
+    c = orc.Md5Ctx()
+    orc.lib().orc_md5_init(ctypes.byref(c))
+    pos = 0
+    while pos < len(data):
+        k = int(rng.integers(0, 3000))
+        orc.lib().orc_md5_update(ctypes.byref(c), data[pos:pos + k], len(data[pos:pos + k]))
+        pos += k
+    orc.lib().orc_md5_final(ctypes.byref(c))
+    assert bytes(c.digest) == ref
+    assert bytes(c.string[:32]).decode() == ref.hex() and c.string[32] == 0
+
+
+def test_pi_tables_two_derivations(orc):
+    words = orc.bf_pi_words()
+    hdr = open(os.path.join(ROOT, "brb_framework_amd/csrc/common/blowfish_pi.h")).read()
+    gen = [int(x, 16) for x in re.findall(r"0x([0-9A-F]{8})U", hdr)]
+    assert len(gen) == 1042
+    assert words == gen
+
+
+def test_blowfish_kat_low_halves(orc, golden):
+    for v in golden["kat"]["blowfish_ecb"]:
+        c = orc.bf_init(bytes.fromhex(v["key"]))
+        p = bytes.fromhex(v["plain"])
+        xl, xr = int.from_bytes(p[:4], "big"), int.from_bytes(p[4:], "big")
+        cl, cr = orc.bf_encrypt(c, xl, xr)
+        ct = bytes.fromhex(v["cipher"])
+        assert cl & 0xFFFFFFFF == int.from_bytes(ct[:4], "big")
+        assert cr & 0xFFFFFFFF == int.from_bytes(ct[4:], "big")
+        # the round trip is exact in all 64 bits (survey [verified])
+        assert orc.bf_encrypt(c, cl, cr, decrypt=True) == (xl, xr)
+
+
+def _libcrypto():
+    try:
+        return ctypes.CDLL("libcrypto.so.3")
+    except OSError:
+        return None
+
+
+def test_blowfish_low_halves_vs_openssl(orc):
+    L = _libcrypto()
+    if L is None:
+        pytest.skip("libcrypto.so.3 not present")
+    rng = np.random.default_rng(7)
+    ks = ctypes.create_string_buffer(8192)
+    for t in range(40):
+        key = rng.integers(0, 256, int(rng.integers(1, 57)), dtype=np.uint8).tobytes()
+        L.BF_set_key(ks, len(key), key)
+        c = orc.bf_init(key)
+        for _ in range(8):
+            pt = rng.integers(0, 256, 8, dtype=np.uint8).tobytes()
+            out = ctypes.create_string_buffer(8)
+            L.BF_ecb_encrypt(pt, out, ks, 1)
+            cl, cr = orc.bf_encrypt(c, int.from_bytes(pt[:4], "big"), int.from_bytes(pt[4:], "big"))
+            assert (cl & 0xFFFFFFFF).to_bytes(4, "big") + (cr & 0xFFFFFFFF).to_bytes(4, "big") == out.raw
+
+
+def test_blowfish_high_halves_nonzero(orc):
+    """The reference's 64-bit words carry: high halves of P/S after Init are non-zero (survey)."""
+    c = orc.bf_init(b"brb_framework_k4")
+    hi = [v >> 32 for v in c.P] + [c.S[s][i] >> 32 for s in range(4) for i in range(256)]
+    assert any(hi) and max(max(c.P), max(max(row) for row in c.S)) < (1 << 51)
+
+
+def test_blowfish64_regression(orc, golden):
+    g = golden["blowfish64"]
+    for ctx in g["contexts"]:
+        c = orc.bf_init(bytes.fromhex(ctx["key"]))
+        assert hashlib.sha256(orc.bf_ctx_bytes(c)).hexdigest() == ctx["sha256"]
+    cfg = g["cfg4"]
+    c = orc.bf_init(bytes.fromhex(cfg["key"]))
+    w = workload.gen_words(cfg["seed"], 2 * cfg["pairs"])
+    assert hashlib.sha256(w.tobytes()).hexdigest() == cfg["plain_sha256"]
+    ct = orc.bf_ecb(c, w.copy(), threads=2)
+    assert hashlib.sha256(ct.tobytes()).hexdigest() == cfg["cipher_sha256"]
+    assert np.array_equal(orc.bf_ecb(c, ct, decrypt=True), w)
+
+
+def test_sha1_inplace_quirk(orc, golden):
+    """BrbSha1_Update rewrites full blocks taken straight from `data` (sha1.c:84-90,157-158):
+    for a 200-byte single update, bytes 64..191 change and 0..63 / 192..199 do not."""
+    q = golden["quirks"]["sha1_inplace"]
+    before = bytearray.fromhex(q["input"])
+    msg = bytearray(before)
+    ctx = orc.Sha1Ctx()
+    orc.lib().orc_sha1_init(ctypes.byref(ctx))
+    orc.lib().orc_sha1_update(ctypes.byref(ctx), (ctypes.c_uint8 * 200).from_buffer(msg), 200)
+    dig = ctypes.create_string_buffer(20)
+    orc.lib().orc_sha1_final(ctypes.byref(ctx), dig)
+    assert dig.raw.hex() == q["digest"] == q["hashlib_digest"]
+    assert msg.hex() == q["after_update"]
+    assert msg[:64] == before[:64] and msg[192:] == before[192:]
+    assert msg[64:128] != before[64:128] and msg[128:192] != before[128:192]
+
+
+def test_sha1_count_quirk_model():
+    """sha1.c:151: one Update of len >= 2^29 adds a spurious carry into count[1].  Model check."""
+    def counts(len_):
+        c0 = (len_ << 3) & 0xFFFFFFFF
+        c1 = (1 if c0 < (len_ << 3) else 0) + ((len_ >> 29) & 0xFFFFFFFF)
+        return c0, c1
+    assert counts(1500) == (12000, 0)
+    assert counts((1 << 29) - 1)[1] == 0
+    assert counts(1 << 29) == (0, 2)            # standard SHA-1 would have count[1] == 1
+
+
+def test_membuffer_quirks(orc, golden):
+    """mem_buf.c:1528 keys Encrypt with 4 bytes, :1582 keys Decrypt with 64: the reference's own
+    MemBuffer round trip does not restore the plaintext (survey [verified])."""
+    for m in golden["quirks"]["membuffer"]:
+        enc = bytearray.fromhex(m["plain"])
+        assert orc.membuf_encrypt(enc, m["size"], m["seed"], m["offset"]) == m["enc_size"]
+        assert enc.hex() == m["enc"]
+        dec = bytearray(enc)
+        assert orc.membuf_decrypt(dec, m["enc_size"], m["seed"], m["offset"]) == m["dec_size"]
+        assert dec.hex() == m["dec"]
+    m = golden["quirks"]["membuffer"][2]
+    plain = bytes.fromhex(m["plain"])
+    assert bytes.fromhex(m["dec"])[:m["size"]] != plain[:m["size"]]
+    # decrypting with the ENCRYPT key length (4) restores it
+    key = orc.membuf_key(m["seed"])
+    c4 = orc.bf_init(key, 4)
+    w = np.frombuffer(bytes.fromhex(m["enc"]), dtype=np.uint64).copy()
+    n_pairs = (m["enc_size"] - m["offset"]) // 16
+    dec4 = orc.bf_ecb(c4, w[: 2 * n_pairs].copy(), decrypt=True)
+    assert dec4.tobytes()[:m["size"]] == plain[:m["size"]]
+
+
+def test_generator_numpy_matches_c(orc):
+    for L in (0, 1, 7, 8, 9, 64, 1500):
+        a = workload.gen_records(0x5EED0002, 123, 37, L)
+        b = orc.gen_records(0x5EED0002, 123, 37, L)
+        assert np.array_equal(a, b), L
