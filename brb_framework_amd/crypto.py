@@ -85,6 +85,14 @@ def lib() -> ctypes.CDLL:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C {HERE}` "
                                "(or __graft_entry__.build())")
+        # One HIP runtime per process: the PyTorch wheel bundles its own libamdhip64.so.7 and
+        # libhsa-runtime64.so.1.  Loading torch first lets the dynamic loader resolve this
+        # library's DT_NEEDED libamdhip64.so.7 to that same copy (glibc matches by SONAME);
+        # the other order maps two HSA runtimes and the second sees no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in _SIGNATURES:
             f = getattr(L, name)
