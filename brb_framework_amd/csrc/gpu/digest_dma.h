@@ -1,0 +1,161 @@
+// digest_dma.h -- the fixed-stride, LDS-DMA staged, lane-per-record digest kernel shared by MD5
+// and SHA-1.  `Alg` supplies State, iv(), compress(st, w) on little-endian message words,
+// finish(st, w, t, len) on the padded tail block, and store<ALIGNED>(out, r, st).
+//
+// Persistent waves: wave w digests record groups w, w + W_total, w + 2 W_total, ... (64 records
+// per group, one per lane).  A wave's work is one flat sequence of "stages" (group, block); the
+// LDS ring prefetches P-1 stages ahead ACROSS group boundaries, so only the wave's very first block
+// pays the HBM latency.  Record r's digest = BRB_MD5Init/Update/Final (md5.c:38-168) or
+// BrbSha1_Do (sha1.c:203-216) of data[r * rec_len .. (r + 1) * rec_len).
+#pragma once
+
+#include "dma_stage.h"
+
+namespace brb_digest {
+
+template <class Alg, int WAVES, int P, bool OUT_ALIGNED>
+__global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
+                                                                       uint64_t n_rec, uint8_t *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * P * brb_dma::kSlotBytes];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
+    const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
+    if (wave0 >= n_groups)
+        return;
+    const uint32_t my_groups = uint32_t((n_groups - wave0 + wstride - 1) / wstride);
+
+    uint8_t *my = ring + wv * (P * brb_dma::kSlotBytes);
+    const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(my));
+    const uint32_t lds_last = lds_base + (P - 1) * brb_dma::kSlotBytes;
+    brb_dma::Stager sg;
+    sg.init(rec_len, lane);
+
+    const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
+    const uint32_t nstage = nfull + (t ? 1 : 0);              // staged blocks per group (>= 1)
+    const uint32_t total = my_groups * nstage;                // stages of this wave
+    const bool fast = rec_len >= 64;                          // single-M0 issue (see issue_fast)
+    const uint64_t grp_step = wstride * 64 * rec_len;         // bytes between this wave's groups
+
+    // ---- issue cursor: runs P-1 stages ahead of the compute cursor, across group boundaries.
+    // The descriptor base always points at the block being issued and num_records at the bytes
+    // left to the end of the batch, so the hardware range check (voffset + inst_offset against
+    // num_records) zeroes exactly the bytes past the batch end.
+    uint64_t is_rec = wave0 * 64;                             // first record of the issuing group
+    uint64_t is_left = (n_rec - is_rec) * rec_len;            // bytes from the issue base to the end
+    const uint8_t *is_base = data + is_rec * rec_len;
+    uint32_t is_blk = 0, is_slot = lds_base;
+    uint32_t vq[4];
+    sg.group_offsets(rec_len, uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64), vq);
+    brb_dma::v4i rs = brb_dma::make_rsrc(is_base, is_left);
+    auto issue_next = [&]() {
+        if (fast) {
+            sg.issue_fast(rs, vq, is_slot);
+        } else {
+            const uint32_t n_grp = uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64);
+            sg.issue(is_base, rec_len, n_grp, is_left, is_slot, 0);
+        }
+        is_slot = is_slot == lds_last ? lds_base : is_slot + brb_dma::kSlotBytes;
+        if (++is_blk < nstage) {
+            is_base += 64;
+            is_left -= 64;
+        } else {                                              // next group of this wave
+            is_blk = 0;
+            is_rec += wstride * 64;
+            is_base += grp_step - uint64_t(nstage - 1) * 64;
+            is_left = is_rec < n_rec ? (n_rec - is_rec) * rec_len : 0;
+            if (is_rec < n_rec && n_rec - is_rec < 64)
+                sg.group_offsets(rec_len, uint32_t(n_rec - is_rec), vq);
+        }
+        rs = brb_dma::make_rsrc(is_base, is_left);
+    };
+#pragma unroll
+    for (int i = 0; i < P - 1; i++)
+        if (uint32_t(i) < total)
+            issue_next();
+
+    typename Alg::State st = Alg::iv();
+    uint32_t w[16];
+    uint64_t rb = wave0 * 64;                                  // compute cursor: first record of group
+    uint32_t b_c = 0, slot = lds_base;
+    for (uint32_t s = 0; s < total; s++) {
+        if (s + P - 1 < total) {
+            issue_next();
+            brb_dma::wait_vmcnt<4 * (P - 1)>();
+        } else {
+            brb_dma::wait_vmcnt<0>();
+        }
+        sg.read(reinterpret_cast<const uint8_t *>(my) + (slot - lds_base), w);
+        slot = slot == lds_last ? lds_base : slot + brb_dma::kSlotBytes;
+        if (b_c < nfull)
+            Alg::compress(st, w);
+        if (++b_c < nstage)
+            continue;
+        // ---- last stage of this group: padding, digest, store
+        // `tt` is laundered through an empty asm so that everything derived from it below is
+        // computed here, once per group, instead of being hoisted out of the loop into live SGPRs
+        // (the hoisted form spilled ~200 SGPRs to VGPR lanes).
+        uint32_t tt = t;
+        asm volatile("" : "+s"(tt));
+        // records ending within 3 bytes of the batch end: a staged dword of their tail may
+        // straddle the end of the batch and was range-checked to zero -> re-read byte by byte
+        const uint64_t r = rb + lane;
+        if (tt && r < n_rec && (n_rec - 1 - r) * rec_len < 4) {
+            const uint8_t *a = data + r * rec_len + 64u * nfull;
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++)
+                    if (4 * i + k < tt)
+                        v |= uint32_t(a[4 * i + k]) << (8 * k);
+                w[i] = v;
+            }
+        }
+        // keep the t tail bytes (none if t == 0), place the 0x80 marker, zero the rest
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) {
+            const uint32_t o = 4 * i;
+            const uint32_t keep = tt > o ? (tt - o < 4 ? tt - o : 4) : 0;
+            uint32_t v = w[i] & uint32_t((uint64_t(1) << (8 * keep)) - 1);
+            if (tt >= o && tt < o + 4)
+                v |= 0x80u << (8 * (tt - o));
+            w[i] = v;
+        }
+        Alg::finish(st, w, t, rec_len);
+        if (r < n_rec)
+            Alg::template store<OUT_ALIGNED>(out, r, st);
+        st = Alg::iv();
+        b_c = 0;
+        rb += wstride * 64;
+    }
+}
+
+// Host-side launch.  Ring depth 3: two blocks in flight cover the HBM latency at one wave per
+// SIMD, and a short ring keeps the cold start short (tools/mb/md5_dma_stamps.hip: first block
+// 7.2K cycles at P=3, 14K at P=8, same steady state).  Grid: one 4-wave workgroup per CU per
+// "round" of resident waves, at most 3 workgroups per CU (48 KiB LDS each), persistent beyond.
+inline bool dma_supported(uint32_t rec_len)
+{
+    return rec_len > 0 && uint64_t(rec_len) * 64 + 64 < (uint64_t(1) << 31);
+}
+
+template <class Alg>
+hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
+                            hipStream_t s)
+{
+    constexpr int W = 4, P = 3;
+    const uint64_t groups = (n_rec + 63) / 64;
+    const uint64_t wgs_needed = (groups + W - 1) / W;
+    const uint64_t cap = 256 * 3;                              // CUs x resident workgroups per CU
+    const unsigned g = unsigned(wgs_needed < cap ? wgs_needed : cap);
+    if (out_al)
+        digest_fixed_dma_kernel<Alg, W, P, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    else
+        digest_fixed_dma_kernel<Alg, W, P, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    return hipGetLastError();
+}
+
+}  // namespace brb_digest

@@ -5,9 +5,12 @@
 // one-block software prefetch; the record's 16 message words are consumed straight from VGPRs.
 // Digest of record r = BRB_MD5Init + BRB_MD5Update(record) + BRB_MD5Final (md5.c:38-168).
 #include "brb_kernels.h"
+#include "digest_dma.h"
 #include "md5_device.h"
 
 namespace {
+
+struct Md5Alg;
 
 struct Out16 {
     template <bool ALIGNED>
@@ -19,6 +22,15 @@ struct Out16 {
         else
             __builtin_memcpy(out + 16 * r, &v, 16);
     }
+};
+
+struct Md5Alg {
+    using State = Md5State;
+    static BRB_DEV State iv() { return md5_iv(); }
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress(st, w); }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { md5_finish(st, w, t, len); }
+    template <bool ALIGNED>
+    static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st) { Out16::store<ALIGNED>(out, r, st); }
 };
 
 // Fixed-stride records, record base 4-byte aligned (data 4-aligned and rec_len % 4 == 0).
@@ -105,6 +117,8 @@ hipError_t launch_md5_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n_re
     const bool out_al = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     const bool in_a4 = (reinterpret_cast<uintptr_t>(data) & 3) == 0 && (rec_len & 3) == 0;
     const unsigned g = grid_for(n_rec);
+    if (brb_digest::dma_supported(rec_len))
+        return brb_digest::launch_fixed_dma<Md5Alg>(data, rec_len, n_rec, out, out_al, s);
     if (in_a4) {
         if (out_al)
             md5_fixed_a4_kernel<kBlock, true><<<g, kBlock, 0, s>>>(data, rec_len, n_rec, out);

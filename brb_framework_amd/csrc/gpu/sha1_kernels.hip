@@ -2,6 +2,7 @@
 // Digest of record r = BrbSha1_Do(record) (libbrb_core/crypto/sha1.c:203-216): 20 raw bytes,
 // big-endian state words (sha1.c:185-188).
 #include "brb_kernels.h"
+#include "digest_dma.h"
 #include "sha1_device.h"
 
 namespace {
@@ -21,6 +22,21 @@ BRB_DEV void store20(uint8_t *out, uint64_t r, const Sha1State &st)
         __builtin_memcpy(o, v, 20);
     }
 }
+
+struct Sha1Alg {
+    using State = Sha1State;
+    static BRB_DEV State iv() { return sha1_iv(); }
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16])
+    {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            w[i] = __builtin_bswap32(w[i]);
+        sha1_compress(st, w);
+    }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { sha1_finish(st, w, t, len); }
+    template <bool ALIGNED>
+    static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st) { store20<ALIGNED>(out, r, st); }
+};
 
 template <int BLOCK, bool OUT_ALIGNED>
 __global__ __launch_bounds__(BLOCK) void sha1_fixed_a4_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
@@ -106,6 +122,8 @@ hipError_t launch_sha1_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n_r
     const bool out_al = (reinterpret_cast<uintptr_t>(out) & 3) == 0;
     const bool in_a4 = (reinterpret_cast<uintptr_t>(data) & 3) == 0 && (rec_len & 3) == 0;
     const unsigned g = grid_for(n_rec);
+    if (brb_digest::dma_supported(rec_len))
+        return brb_digest::launch_fixed_dma<Sha1Alg>(data, rec_len, n_rec, out, out_al, s);
     if (in_a4) {
         if (out_al)
             sha1_fixed_a4_kernel<kBlock, true><<<g, kBlock, 0, s>>>(data, rec_len, n_rec, out);

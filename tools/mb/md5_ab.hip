@@ -1,0 +1,145 @@
+// md5_ab.hip -- interleaved A/B of MD5 batch kernel variants on cfg2 (65536 x 1500 B), one process
+// (cdna_hip_programming.md rule 24).  Variants share the product's device code.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../brb_framework_amd/csrc/gpu md5_ab.hip -o md5ab
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "digest_dma.h"
+#include "md5_device.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+// the "SGPR K" form of the step: hipcc keeps the 64 constants in SGPRs for v_add3
+#define STEP_SK(F, a, b, c, d, m, k, s) (a) = (b) + rotl<s>((a) + F((b), (c), (d)) + ((m) + (k)))
+BRB_DEV void md5_compress_sk(Md5State &st, const uint32_t (&m)[16])
+{
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+#define F1 BRB_MD5_F1
+#define F2 BRB_MD5_F2
+#define F3 BRB_MD5_F3
+#define F4 BRB_MD5_F4
+    STEP_SK(F1, a, b, c, d, m[0], 0xd76aa478u, 7); STEP_SK(F1, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    STEP_SK(F1, c, d, a, b, m[2], 0x242070dbu, 17); STEP_SK(F1, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    STEP_SK(F1, a, b, c, d, m[4], 0xf57c0fafu, 7); STEP_SK(F1, d, a, b, c, m[5], 0x4787c62au, 12);
+    STEP_SK(F1, c, d, a, b, m[6], 0xa8304613u, 17); STEP_SK(F1, b, c, d, a, m[7], 0xfd469501u, 22);
+    STEP_SK(F1, a, b, c, d, m[8], 0x698098d8u, 7); STEP_SK(F1, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    STEP_SK(F1, c, d, a, b, m[10], 0xffff5bb1u, 17); STEP_SK(F1, b, c, d, a, m[11], 0x895cd7beu, 22);
+    STEP_SK(F1, a, b, c, d, m[12], 0x6b901122u, 7); STEP_SK(F1, d, a, b, c, m[13], 0xfd987193u, 12);
+    STEP_SK(F1, c, d, a, b, m[14], 0xa679438eu, 17); STEP_SK(F1, b, c, d, a, m[15], 0x49b40821u, 22);
+    STEP_SK(F2, a, b, c, d, m[1], 0xf61e2562u, 5); STEP_SK(F2, d, a, b, c, m[6], 0xc040b340u, 9);
+    STEP_SK(F2, c, d, a, b, m[11], 0x265e5a51u, 14); STEP_SK(F2, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    STEP_SK(F2, a, b, c, d, m[5], 0xd62f105du, 5); STEP_SK(F2, d, a, b, c, m[10], 0x02441453u, 9);
+    STEP_SK(F2, c, d, a, b, m[15], 0xd8a1e681u, 14); STEP_SK(F2, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    STEP_SK(F2, a, b, c, d, m[9], 0x21e1cde6u, 5); STEP_SK(F2, d, a, b, c, m[14], 0xc33707d6u, 9);
+    STEP_SK(F2, c, d, a, b, m[3], 0xf4d50d87u, 14); STEP_SK(F2, b, c, d, a, m[8], 0x455a14edu, 20);
+    STEP_SK(F2, a, b, c, d, m[13], 0xa9e3e905u, 5); STEP_SK(F2, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    STEP_SK(F2, c, d, a, b, m[7], 0x676f02d9u, 14); STEP_SK(F2, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    STEP_SK(F3, a, b, c, d, m[5], 0xfffa3942u, 4); STEP_SK(F3, d, a, b, c, m[8], 0x8771f681u, 11);
+    STEP_SK(F3, c, d, a, b, m[11], 0x6d9d6122u, 16); STEP_SK(F3, b, c, d, a, m[14], 0xfde5380cu, 23);
+    STEP_SK(F3, a, b, c, d, m[1], 0xa4beea44u, 4); STEP_SK(F3, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    STEP_SK(F3, c, d, a, b, m[7], 0xf6bb4b60u, 16); STEP_SK(F3, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    STEP_SK(F3, a, b, c, d, m[13], 0x289b7ec6u, 4); STEP_SK(F3, d, a, b, c, m[0], 0xeaa127fau, 11);
+    STEP_SK(F3, c, d, a, b, m[3], 0xd4ef3085u, 16); STEP_SK(F3, b, c, d, a, m[6], 0x04881d05u, 23);
+    STEP_SK(F3, a, b, c, d, m[9], 0xd9d4d039u, 4); STEP_SK(F3, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    STEP_SK(F3, c, d, a, b, m[15], 0x1fa27cf8u, 16); STEP_SK(F3, b, c, d, a, m[2], 0xc4ac5665u, 23);
+    STEP_SK(F4, a, b, c, d, m[0], 0xf4292244u, 6); STEP_SK(F4, d, a, b, c, m[7], 0x432aff97u, 10);
+    STEP_SK(F4, c, d, a, b, m[14], 0xab9423a7u, 15); STEP_SK(F4, b, c, d, a, m[5], 0xfc93a039u, 21);
+    STEP_SK(F4, a, b, c, d, m[12], 0x655b59c3u, 6); STEP_SK(F4, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    STEP_SK(F4, c, d, a, b, m[10], 0xffeff47du, 15); STEP_SK(F4, b, c, d, a, m[1], 0x85845dd1u, 21);
+    STEP_SK(F4, a, b, c, d, m[8], 0x6fa87e4fu, 6); STEP_SK(F4, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    STEP_SK(F4, c, d, a, b, m[6], 0xa3014314u, 15); STEP_SK(F4, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    STEP_SK(F4, a, b, c, d, m[4], 0xf7537e82u, 6); STEP_SK(F4, d, a, b, c, m[11], 0xbd3af235u, 10);
+    STEP_SK(F4, c, d, a, b, m[2], 0x2ad7d2bbu, 15); STEP_SK(F4, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st.a += a; st.b += b; st.c += c; st.d += d;
+}
+
+struct AlgLit {      // product compress (m + K as a literal VOP2 add)
+    using State = Md5State;
+    static BRB_DEV State iv() { return md5_iv(); }
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress(st, w); }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { md5_finish(st, w, t, len); }
+    template <bool A> static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st)
+    { reinterpret_cast<uint4 *>(out)[r] = make_uint4(st.a, st.b, st.c, st.d); }
+};
+struct AlgSK : AlgLit {
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress_sk(st, w); }
+};
+struct AlgSched : AlgLit {
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress_sched(st, w); }
+};
+
+struct AlgNull : AlgLit {   // memory-side floor: consume the staged words with 16 xors
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16])
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) x ^= w[i];
+        st.a ^= x;
+    }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t, uint64_t) { st.b ^= w[0]; }
+};
+
+using Kern = void (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *);
+
+int main(int argc, char **argv)
+{
+    const uint32_t L = argc > 2 ? atoi(argv[2]) : 1500;
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 65536;
+    std::vector<uint8_t> h(n * L);
+    uint64_t x = 99;
+    for (auto &c : h) { x = x * 6364136223846793005ull + 1442695040888963407ull; c = uint8_t(x >> 56); }
+    const int nrot = std::max<int>(2, int(700e6 / double(n * L)) + 1);
+    std::vector<uint8_t *> d(nrot);
+    for (int i = 0; i < nrot; i++) {
+        CK(hipMalloc(&d[i], n * L + 8192));
+        CK(hipMemcpy(d[i], h.data(), n * L, hipMemcpyHostToDevice));
+    }
+    uint8_t *o;
+    CK(hipMalloc(&o, n * 16));
+    struct V { const char *name; Kern k; int waves; int cap; };
+    std::vector<V> vs = {
+        {"persistent P3 lit-K", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 3, true>, 4, 768},
+        {"persistent P3 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, true>, 4, 768},
+        {"persistent P3 sched", brb_digest::digest_fixed_dma_kernel<AlgSched, 4, 3, true>, 4, 768},
+        {"persistent P2 lit-K", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, true>, 4, 1280},
+        {"persistent P2 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, true>, 4, 1280},
+        {"persistent P4 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 4, true>, 4, 512},
+        {"DMA only P3 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, true>, 4, 768},
+        {"DMA only P4 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 4, true>, 4, 512},
+        {"DMA only P2 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, true>, 4, 1280},
+    };
+    std::vector<uint8_t> ref(n * 16), got(n * 16);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    std::vector<std::vector<float>> t(vs.size());
+    int it = 0;
+    for (int rep = 0; rep < 25; rep++)
+        for (size_t v = 0; v < vs.size(); v++) {
+            const uint64_t groups = (n + 63) / 64, need = (groups + vs[v].waves - 1) / vs[v].waves;
+            const unsigned grid = unsigned(std::min<uint64_t>(need, vs[v].cap));
+            hipEventRecord(e0);
+            hipLaunchKernelGGL(vs[v].k, dim3(grid), dim3(64 * vs[v].waves), 0, 0, d[it++ % nrot], L, n, o);
+            hipEventRecord(e1);
+            CK(hipEventSynchronize(e1));
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            t[v].push_back(ms * 1e3f);
+            if (rep == 0) {
+                CK(hipMemcpy(v == 0 ? ref.data() : got.data(), o, n * 16, hipMemcpyDeviceToHost));
+                if (v && strncmp(vs[v].name, "DMA only", 8) && memcmp(ref.data(), got.data(), n * 16))
+                    printf("MISMATCH %s\n", vs[v].name);
+            }
+        }
+    printf("n=%llu L=%u\n", (unsigned long long)n, L);
+    for (size_t v = 0; v < vs.size(); v++) {
+        std::sort(t[v].begin(), t[v].end());
+        const float med = t[v][t[v].size() / 2];
+        printf("%-28s median %8.2f us  min %8.2f us  %6.0f GB/s\n", vs[v].name, med, t[v][0], n * L / (med * 1e-6) / 1e9);
+    }
+    return 0;
+}
