@@ -11,8 +11,8 @@ Honesty rules applied here:
     >= 640 MB > the 256 MiB Infinity Cache), so the kernel streams from HBM, not from L3;
   * the timed region is K back-to-back steps, each one C-ABI call (ctypes, arguments resolved
     beforehand), between barrier + synchronize on both sides; value is the whole-job rate (all ranks' bytes / max over ranks of the wall time);
-  * roofline.achieved uses the kernel's own average duration from HIP events recorded on the
-    stream the kernel runs on; digests of the last step are spot-checked against hashlib.
+  * roofline.achieved = bytes per launch / (HIP-event time of the timed region on the launch
+    stream / K); digests of the last step are spot-checked against hashlib.
 
 Other workloads for DESIGN.md: --config 3 (1 Mi x 64 B MD5), --config 4 (1 GiB Blowfish enc+dec),
 --op sha1.  Run `python bench.py --help`.
@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--op", default="md5", choices=["md5", "sha1"])
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the timed steps alternate over")
+    ap.add_argument("--two-stream", action="store_true", help="also time the steps over 2 streams")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-inclusive (PCIe) measurement")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
@@ -132,28 +133,22 @@ def main():
 def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     """K steps between barrier + synchronize on both sides; step k is enqueued on
     streams[k % len(streams)] straight through the C ABI (pre-resolved ctypes arguments, so the
-    host enqueues faster than the GPU drains and no per-step event sits between kernels)."""
+    host enqueues faster than the GPU drains).  HIP events on the launch stream bracket the same
+    region (one pair, nothing between kernels).  Returns (wall seconds max over ranks,
+    event-timed seconds on stream 0)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record(streams[0])
     for k in range(n_steps):
         j = k % len(streams)
         launch(k, streams[j], j)
+    e1.record(streams[0])
     torch.cuda.synchronize()
     barrier()
-    return max_over_ranks(time.perf_counter() - t0)
-
-
-def kernel_durations(launch, n, stream, torch):
-    """Per-launch HIP-event pairs on the launch stream -> sorted kernel durations (ms)."""
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
-    torch.cuda.synchronize()
-    for k in range(n):
-        ev[k][0].record(stream)
-        launch(k, stream)
-        ev[k][1].record(stream)
-        ev[k][1].synchronize()          # one launch at a time: nothing overlaps the measured kernel
-    return sorted(a.elapsed_time(b) for a, b in ev)
+    wall = max_over_ranks(time.perf_counter() - t0)
+    return wall, e0.elapsed_time(e1) / 1e3
 
 
 def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log):
@@ -210,11 +205,12 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         launch(k, all_streams[k % len(all_streams)], k % len(all_streams))
     torch.cuda.synchronize()
     main_streams = [stream] if n_streams == 1 else side[:n_streams]
-    wall = timed_steps(lambda k, s, j: launch_raw(k + args.warmup, s, j), args.steps, main_streams,
-                       barrier, max_over_ranks, torch)
-    kern_ms = kernel_durations(launch, min(args.steps, 50), stream, torch)
-    # throughput with two batches in flight (the same steps over two HIP streams), beside the main number
-    wall2 = timed_steps(launch_raw, args.steps, side[:2], barrier, max_over_ranks, torch)
+    wall, ev_s = timed_steps(lambda k, s, j: launch_raw(k + args.warmup, s, j), args.steps, main_streams,
+                             barrier, max_over_ranks, torch)
+    wall2 = None
+    if args.two_stream:
+        # the same K steps alternating over two HIP streams (two batches in flight)
+        wall2, _ = timed_steps(launch_raw, args.steps, side[:2], barrier, max_over_ranks, torch)
     out = outs[0]
 
     # spot-check the last step's digests against hashlib (stdlib, independent of this repo)
@@ -226,8 +222,9 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     total_bytes = n_global * L * args.steps
     gib_s = total_bytes / wall / 2**30
     mrec_s = n_global * args.steps / wall / 1e6
-    avg_kern_s = sum(kern_ms) / len(kern_ms) / 1e3
-    med_kern_s = kern_ms[len(kern_ms) // 2] / 1e3
+    # per-launch duration from the events around the timed region (single stream: launches run back
+    # to back, so this is the kernel time plus the ~2 us dependent-kernel boundary)
+    avg_kern_s = ev_s / args.steps
     achieved = n_rank * L / avg_kern_s / 1e9
     traffic = load_traffic(args.pmc_summary, f"cfg{cfg_id}_{args.op}")
     result = {
@@ -250,19 +247,21 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
                    "parallelism": f"record-shard x{world}, no collective"},
         "mrecords_per_s": round(mrec_s, 3),
         "streams": n_streams,
-        "two_stream_throughput": {"value": round(n_global * L * args.steps / wall2 / 2**30, 2), "unit": "GiB/s",
-                                  "mrecords_per_s": round(n_global * args.steps / wall2 / 1e6, 3),
-                                  "note": "same K steps, alternating over 2 HIP streams (2 batches in flight)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel_us_avg": round(avg_kern_s * 1e6, 2), "kernel_us_median": round(med_kern_s * 1e6, 2),
-                     "bytes_per_launch": n_rank * L},
+                     "launch_us_avg": round(avg_kern_s * 1e6, 2), "bytes_per_launch": n_rank * L,
+                     "timing": "HIP events on the launch stream around the K back-to-back steps / K"},
     }
+    if wall2 is not None:
+        result["two_stream_throughput"] = {
+            "value": round(n_global * L * args.steps / wall2 / 2**30, 2), "unit": "GiB/s",
+            "mrecords_per_s": round(n_global * args.steps / wall2 / 1e6, 3),
+            "note": "same K steps alternating over 2 HIP streams (2 batches in flight)"}
     if world == 1 and not args.no_pcie:
         result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, dev, stream, log)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_digest(args, host, L, n_rank, log)
-    log(f"[bench] kernel avg {avg_kern_s * 1e6:.1f} us -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.1%} of HBM peak)")
+    log(f"[bench] launch avg {avg_kern_s * 1e6:.1f} us -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.1%} of HBM peak)")
     return result
 
 
@@ -337,15 +336,14 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
     for k in range(args.warmup):
         launch(k, stream)
     torch.cuda.synchronize()
-    wall = timed_steps(launch, args.steps, [stream], barrier, max_over_ranks, torch)
-    kern_ms = kernel_durations(launch, min(args.steps, 20), stream, torch)
+    wall, ev_s = timed_steps(launch, args.steps, [stream], barrier, max_over_ranks, torch)
     assert torch.equal(d, d0), "Blowfish round trip did not restore the plaintext"
     # one encrypt-only check against the oracle on a sample record
     brb.blowfish_encrypt_batch(cdev, d, n_blocks)
     wpr = cfg["rec_len"] // 8
     got = d[:wpr].cpu().numpy().view(np.uint64)
     assert np.array_equal(got, oracle.bf_ecb(oracle.bf_init(workload.CFG4_KEY), w[:wpr].copy()))
-    step_s = sum(kern_ms) / len(kern_ms) / 1e3
+    step_s = ev_s / args.steps
     plain = n_words * 8
     result = {
         "metric": "GiB/s of plaintext per Blowfish encrypt+decrypt round trip (cfg4)",
@@ -359,7 +357,8 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
                    "parallelism": f"record-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(4 * plain / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(4 * plain / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic(args.pmc_summary, "cfg4_blowfish"),
+                     "traffic": (2 * load_traffic(args.pmc_summary, "cfg4_blowfish")
+                                 if load_traffic(args.pmc_summary, "cfg4_blowfish") else None),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": 4 * plain,
                      "note": "algorithmic bytes = read + write of the plaintext in each direction"},
     }

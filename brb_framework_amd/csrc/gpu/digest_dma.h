@@ -13,11 +13,12 @@
 
 namespace brb_digest {
 
-template <class Alg, int WAVES, int P, bool OUT_ALIGNED>
+template <class Alg, int WAVES, int P, int BPS, bool OUT_ALIGNED>
 __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
                                                                        uint64_t n_rec, uint8_t *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * P * brb_dma::kSlotBytes];
+    using SG = brb_dma::Stager<BPS>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * P * SG::SLOT];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
@@ -27,47 +28,43 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         return;
     const uint32_t my_groups = uint32_t((n_groups - wave0 + wstride - 1) / wstride);
 
-    uint8_t *my = ring + wv * (P * brb_dma::kSlotBytes);
+    uint8_t *my = ring + wv * (P * SG::SLOT);
     const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(my));
-    const uint32_t lds_last = lds_base + (P - 1) * brb_dma::kSlotBytes;
-    brb_dma::Stager sg;
-    sg.init(rec_len, lane);
+    const uint32_t lds_last = lds_base + (P - 1) * SG::SLOT;
 
     const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
-    const uint32_t nstage = nfull + (t ? 1 : 0);              // staged blocks per group (>= 1)
+    const uint32_t nblk = nfull + (t ? 1 : 0);                // blocks holding record bytes (>= 1)
+    const uint32_t nstage = (nblk + BPS - 1) / BPS;           // stages per group
     const uint32_t total = my_groups * nstage;                // stages of this wave
-    const bool fast = rec_len >= 64;                          // single-M0 issue (see issue_fast)
+    const bool fast = rec_len >= 64 * BPS;                    // inst_offset form of the issue
     const uint64_t grp_step = wstride * 64 * rec_len;         // bytes between this wave's groups
 
     // ---- issue cursor: runs P-1 stages ahead of the compute cursor, across group boundaries.
-    // The descriptor base always points at the block being issued and num_records at the bytes
-    // left to the end of the batch, so the hardware range check (voffset + inst_offset against
-    // num_records) zeroes exactly the bytes past the batch end.
+    // The descriptor base points at the stage being issued and num_records at the bytes left to
+    // the end of the batch, so the range check zeroes exactly the bytes past the batch end.
     uint64_t is_rec = wave0 * 64;                             // first record of the issuing group
-    uint64_t is_left = (n_rec - is_rec) * rec_len;            // bytes from the issue base to the end
+    uint64_t is_left = (n_rec - is_rec) * rec_len;
     const uint8_t *is_base = data + is_rec * rec_len;
-    uint32_t is_blk = 0, is_slot = lds_base;
-    uint32_t vq[4];
-    sg.group_offsets(rec_len, uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64), vq);
+    uint32_t is_stage = 0, is_slot = lds_base;
+    SG sg;
+    sg.init(rec_len, uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64), lane, fast);
     brb_dma::v4i rs = brb_dma::make_rsrc(is_base, is_left);
     auto issue_next = [&]() {
-        if (fast) {
-            sg.issue_fast(rs, vq, is_slot);
-        } else {
-            const uint32_t n_grp = uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64);
-            sg.issue(is_base, rec_len, n_grp, is_left, is_slot, 0);
-        }
-        is_slot = is_slot == lds_last ? lds_base : is_slot + brb_dma::kSlotBytes;
-        if (++is_blk < nstage) {
-            is_base += 64;
-            is_left -= 64;
-        } else {                                              // next group of this wave
-            is_blk = 0;
+        if (fast)
+            sg.issue_fast(rs, is_slot);
+        else
+            sg.issue_slow(rs, is_slot);
+        is_slot = is_slot == lds_last ? lds_base : is_slot + SG::SLOT;
+        if (++is_stage < nstage) {
+            is_base += SG::S;
+            is_left -= SG::S;
+        } else {                                              // this wave's next group
+            is_stage = 0;
             is_rec += wstride * 64;
-            is_base += grp_step - uint64_t(nstage - 1) * 64;
+            is_base += grp_step - uint64_t(nstage - 1) * SG::S;
             is_left = is_rec < n_rec ? (n_rec - is_rec) * rec_len : 0;
             if (is_rec < n_rec && n_rec - is_rec < 64)
-                sg.group_offsets(rec_len, uint32_t(n_rec - is_rec), vq);
+                sg.group_offsets(rec_len, uint32_t(n_rec - is_rec), fast);
         }
         rs = brb_dma::make_rsrc(is_base, is_left);
     };
@@ -79,19 +76,25 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
     typename Alg::State st = Alg::iv();
     uint32_t w[16];
     uint64_t rb = wave0 * 64;                                  // compute cursor: first record of group
-    uint32_t b_c = 0, slot = lds_base;
+    uint32_t cs = 0, slot = lds_base;
     for (uint32_t s = 0; s < total; s++) {
         if (s + P - 1 < total) {
             issue_next();
-            brb_dma::wait_vmcnt<4 * (P - 1)>();
+            brb_dma::wait_vmcnt<SG::NI * (P - 1)>();
         } else {
             brb_dma::wait_vmcnt<0>();
         }
-        sg.read(reinterpret_cast<const uint8_t *>(my) + (slot - lds_base), w);
-        slot = slot == lds_last ? lds_base : slot + brb_dma::kSlotBytes;
-        if (b_c < nfull)
-            Alg::compress(st, w);
-        if (++b_c < nstage)
+        const uint8_t *sp = my + (slot - lds_base);
+        slot = slot == lds_last ? lds_base : slot + SG::SLOT;
+        const uint32_t b0 = cs * BPS;
+#pragma unroll
+        for (uint32_t j = 0; j < BPS; j++) {
+            if (b0 + j < nfull) {
+                sg.read(sp, j, w);
+                Alg::compress(st, w);
+            }
+        }
+        if (++cs < nstage)
             continue;
         // ---- last stage of this group: padding, digest, store
         // `tt` is laundered through an empty asm so that everything derived from it below is
@@ -99,6 +102,13 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         // (the hoisted form spilled ~200 SGPRs to VGPR lanes).
         uint32_t tt = t;
         asm volatile("" : "+s"(tt));
+        if (tt) {
+            sg.read(sp, nfull - b0, w);                       // the tail block of this stage
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++)
+                w[i] = 0;
+        }
         // records ending within 3 bytes of the batch end: a staged dword of their tail may
         // straddle the end of the batch and was range-checked to zero -> re-read byte by byte
         const uint64_t r = rb + lane;
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
                 w[i] = v;
             }
         }
-        // keep the t tail bytes (none if t == 0), place the 0x80 marker, zero the rest
+        // keep the t tail bytes, place the 0x80 marker, zero the rest
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++) {
             const uint32_t o = 4 * i;
@@ -128,15 +138,12 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         if (r < n_rec)
             Alg::template store<OUT_ALIGNED>(out, r, st);
         st = Alg::iv();
-        b_c = 0;
+        cs = 0;
         rb += wstride * 64;
     }
 }
 
-// Host-side launch.  Ring depth 3: two blocks in flight cover the HBM latency at one wave per
-// SIMD, and a short ring keeps the cold start short (tools/mb/md5_dma_stamps.hip: first block
-// 7.2K cycles at P=3, 14K at P=8, same steady state).  Grid: one 4-wave workgroup per CU per
-// "round" of resident waves, at most 3 workgroups per CU (48 KiB LDS each), persistent beyond.
+// Host-side launch.
 inline bool dma_supported(uint32_t rec_len)
 {
     return rec_len > 0 && uint64_t(rec_len) * 64 + 64 < (uint64_t(1) << 31);
@@ -146,15 +153,27 @@ template <class Alg>
 hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
                             hipStream_t s)
 {
-    constexpr int W = 4, P = 3;
+    // Shapes measured with tools/mb/md5_ab.hip (interleaved, one process):
+    //  * records > 64 B: 128-byte stages, ring of 2 (16 KiB per wave, 64 KiB per 4-wave workgroup,
+    //    2 workgroups per CU): 1 Mi x 1500 B 335 us vs 388 us with 64-byte stages;
+    //  * records <= 64 B (one block + padding): 64-byte stages, ring of 3, 3 workgroups per CU.
+    // Persistent beyond the resident grid (waves loop over groups of 64 records).
+    constexpr int W = 4;
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs_needed = (groups + W - 1) / W;
-    const uint64_t cap = 256 * 3;                              // CUs x resident workgroups per CU
-    const unsigned g = unsigned(wgs_needed < cap ? wgs_needed : cap);
-    if (out_al)
-        digest_fixed_dma_kernel<Alg, W, P, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
-    else
-        digest_fixed_dma_kernel<Alg, W, P, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    if (rec_len > 64) {
+        const unsigned g = unsigned(wgs_needed < 512 ? wgs_needed : 512);
+        if (out_al)
+            digest_fixed_dma_kernel<Alg, W, 2, 2, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+        else
+            digest_fixed_dma_kernel<Alg, W, 2, 2, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    } else {
+        const unsigned g = unsigned(wgs_needed < 768 ? wgs_needed : 768);
+        if (out_al)
+            digest_fixed_dma_kernel<Alg, W, 3, 1, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+        else
+            digest_fixed_dma_kernel<Alg, W, 3, 1, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    }
     return hipGetLastError();
 }
 

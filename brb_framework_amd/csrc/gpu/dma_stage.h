@@ -1,25 +1,29 @@
 // dma_stage.h -- LDS-DMA staging of fixed-stride records for the lane-per-record digest kernels.
 //
-// A wave digests groups of 64 consecutive records, one record per lane.  Message block `blk` of
-// all 64 records of a group (4 KiB) is brought into a private LDS ring slot by four
-// `buffer_load_dwordx4 ... lds` instructions (LDS-DMA: no VGPR destination, no ds_write,
-// unaligned sources allowed).  One instruction covers 16 records x 64 contiguous bytes, so L2/HBM
-// see 64-byte segments instead of the 16-byte per-lane scatter of direct loads.  The LDS image is
-// lane-linear per instruction, so the bank swizzle is applied to the SOURCE address
-// (cdna_hip_programming.md rule 21): slot j of instruction q holds record 16q + j/4, chunk
-// (j & 3) ^ ((j >> 4) & 3); lane r then reads chunk c of its record at
-//   r * 64 + (c ^ ((r >> 2) & 3)) * 16
-// which is conflict-free for ds_read_b128's four 16-lane groups (SQ_LDS_BANK_CONFLICT = 0).
+// A wave digests groups of 64 consecutive records, one record per lane.  A "stage" brings S bytes
+// (S = 64 * BPS, BPS message blocks) of all 64 records of a group into a private LDS ring slot with
+// 4 * BPS `buffer_load_dwordx4 ... lds` instructions (LDS-DMA: no VGPR destination, no ds_write,
+// unaligned sources allowed).  One instruction covers 1024 / S records x S contiguous bytes.
+// Why S = 128 (BPS = 2) and not 64: records of 1500 B are only 4-byte aligned, so a 64-byte piece
+// straddles two 64-byte memory sectors; at S = 64 the staging alone streams at 4.5 TB/s on a
+// 1 Mi-record batch, at S = 128 at 5.5 TB/s, against 6.4 TB/s for a contiguous copy
+// (tools/mb/dma_pattern.hip, 1 048 576 x 1500 B).
 //
-// The group base is a buffer descriptor (SGPRs), each lane's record row + chunk a 32-bit voffset,
-// the block index the scalar soffset: staging costs no VALU work per block.
+// The LDS image is lane-linear per instruction, so the bank swizzle is applied to the SOURCE
+// address (cdna_hip_programming.md rule 21): a slot row is one record's S bytes = G = S / 16
+// granules of 16 B; logical granule k of record r sits at physical granule k ^ f(r) with
+//   f(r) = (r >> 2) & 3  (G = 4)     f(r) = (r >> 1) & 7  (G = 8)
+// which makes ds_read_b128 of one granule by all 64 lanes conflict-free (SQ_LDS_BANK_CONFLICT = 0).
+//
+// The stage base is a buffer descriptor (SGPRs) whose num_records is the byte count to the end of
+// the batch, each lane's record row + granule a 32-bit voffset: staging costs no VALU per stage,
+// and the hardware range check (voffset + inst_offset against num_records) returns zeros for bytes
+// past the batch end instead of faulting.
 #pragma once
 
 #include "brb_gpu_common.h"
 
 namespace brb_dma {
-
-constexpr int kSlotBytes = 4096;     // one 64-byte block of 64 records
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
@@ -35,97 +39,93 @@ BRB_DEV v4i make_rsrc(const uint8_t *base, uint64_t extent)
     return r;
 }
 
+template <int BPS>
 struct Stager {
-    uint32_t voff[4];                // per-lane source offset of instruction q (record row + chunk)
-    uint32_t lane_row;               // this lane's record row inside a slot
-    uint32_t chunk, lane;
+    static constexpr int S = 64 * BPS;          // bytes of one record per stage
+    static constexpr int G = S / 16;            // 16-byte granules per record row
+    static constexpr int NI = 4 * BPS;          // DMA instructions per stage (1 KiB each)
+    static constexpr int RPI = 1024 / S;        // records per instruction
+    static constexpr int SLOT = 64 * S;         // LDS bytes per stage
+    static_assert(BPS == 1 || BPS == 2, "swizzle defined for 64- and 128-byte rows");
 
-    BRB_DEV void init(uint32_t stride, uint32_t lane_)
+    uint32_t vq[NI];                 // per-lane source offset of instruction q (minus 1024 (q % 4))
+    uint32_t lane;
+
+    static BRB_DEV uint32_t swz(uint32_t r) { return G == 4 ? (r >> 2) & 3 : (r >> 1) & 7; }
+
+    // Offsets for a group of n_grp records (n_grp < 64: lanes past the end re-read the last one).
+    // fast (stride >= 128): instruction q carries inst_offset 1024 (q % 4), cancelled here.
+    BRB_DEV void group_offsets(uint32_t stride, uint32_t n_grp, bool fast)
+    {
+        const uint32_t last = n_grp - 1, sub = lane / G, gran = lane % G;
+#pragma unroll
+        for (int q = 0; q < NI; q++) {
+            const uint32_t row = uint32_t(q * RPI) + sub;                  // LDS slot row
+            const uint32_t rec = min(row, last);
+            const uint32_t logical = gran ^ swz(row);
+            vq[q] = rec * stride + logical * 16 - (fast ? 1024u * (q & 3) : 0u);
+        }
+    }
+
+    BRB_DEV void init(uint32_t stride, uint32_t n_grp, uint32_t lane_, bool fast)
     {
         lane = lane_;
-        chunk = (lane & 3) ^ ((lane >> 4) & 3);
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            voff[q] = (16 * q + (lane >> 2)) * stride + chunk * 16;
-        lane_row = lane * 64;
+        group_offsets(stride, n_grp, fast);
     }
 
-    // Issue the 4 DMAs of block `blk` of the group at `base` (n_grp records, `extent` bytes to the
-    // end of the batch) into the LDS slot at byte address `slot_lds` (wave-uniform).
-    // Inline asm on purpose: hipcc, seeing an LDS-DMA builtin, drains the whole ring with
-    // vmcnt(0) before every ds_read; the counted waits are placed by hand instead (wait_vmcnt).
-    // M0 is saved and restored inside the statement (it is compiler-reserved).
-    BRB_DEV void issue(const uint8_t *base, uint32_t stride, uint32_t n_grp, uint64_t extent, uint32_t slot_lds,
-                       uint32_t blk) const
+    // Issue one stage into the LDS slot at byte address slot_lds (wave-uniform).  Inline asm on
+    // purpose: hipcc, seeing an LDS-DMA builtin, drains the whole ring with vmcnt(0) before every
+    // ds_read; the counted waits are placed by hand instead (wait_vmcnt).  M0 (the LDS base of a
+    // DMA) is compiler-reserved, so it is saved and restored inside the statement.
+    BRB_DEV void issue_fast(const v4i &rsrc, uint32_t slot_lds) const
     {
-        const v4i rsrc = make_rsrc(base, extent);
-        uint32_t v0 = voff[0], v1 = voff[1], v2 = voff[2], v3 = voff[3];
-        if (n_grp < 64) {                                    // partial last group: re-read a valid record
-            const uint32_t last = n_grp - 1, r = lane >> 2, c16 = chunk * 16;
-            v0 = min(r, last) * stride + c16;
-            v1 = min(16 + r, last) * stride + c16;
-            v2 = min(32 + r, last) * stride + c16;
-            v3 = min(48 + r, last) * stride + c16;
+#pragma unroll
+        for (int h = 0; h < BPS; h++) {
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %6\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %5, 0 offen lds\n\t"
+                "buffer_load_dwordx4 %2, %5, 0 offen offset:1024 lds\n\t"
+                "buffer_load_dwordx4 %3, %5, 0 offen offset:2048 lds\n\t"
+                "buffer_load_dwordx4 %4, %5, 0 offen offset:3072 lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(vq[4 * h]), "v"(vq[4 * h + 1]), "v"(vq[4 * h + 2]), "v"(vq[4 * h + 3]), "s"(rsrc),
+                  "s"(slot_lds + 4096u * h)
+                : "memory");
         }
-        const uint32_t soff = __builtin_amdgcn_readfirstlane(blk * 64);
-        const uint32_t m = __builtin_amdgcn_readfirstlane(slot_lds);
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %7\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
-            "s_add_u32 m0, m0, 0x400\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %4, %5, %6 offen lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(v0), "v"(v1), "v"(v2), "v"(v3), "s"(rsrc), "s"(soff), "s"(m)
-            : "memory", "scc");
     }
 
-    // Same as issue(), for stride >= 64: one M0 write per block.  The instruction offset field
-    // (applied to both the LDS destination and the global address) selects the 1 KiB quarter of
-    // the slot; the per-lane voffsets carry -1024 q to cancel it on the global side.
-    BRB_DEV void issue_fast(const v4i &rsrc, const uint32_t (&vq)[4], uint32_t slot_lds) const
+    // Same, one M0 write per instruction (strides below 128, where the inst_offset trick would
+    // need negative voffsets).
+    BRB_DEV void issue_slow(const v4i &rsrc, uint32_t slot_lds) const
     {
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %6\n\t"
-            "s_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %5, 0 offen lds\n\t"
-            "buffer_load_dwordx4 %2, %5, 0 offen offset:1024 lds\n\t"
-            "buffer_load_dwordx4 %3, %5, 0 offen offset:2048 lds\n\t"
-            "buffer_load_dwordx4 %4, %5, 0 offen offset:3072 lds\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "s"(rsrc), "s"(slot_lds)
-            : "memory");
-    }
-
-    // Per-lane voffsets of issue_fast for a group of n_grp records (n_grp < 64: clamp to the last).
-    BRB_DEV void group_offsets(uint32_t stride, uint32_t n_grp, uint32_t (&vq)[4]) const
-    {
-        const uint32_t last = n_grp - 1, r = lane >> 2, c16 = chunk * 16;
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            vq[q] = min(16u * q + r, last) * stride + c16 - 1024u * q;
+        for (int q = 0; q < NI; q++) {
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %3\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(vq[q]), "s"(rsrc), "s"(slot_lds + 1024u * q)
+                : "memory");
+        }
     }
 
-    // Read this lane's 16 little-endian words of the block in `slot`.
-    BRB_DEV void read(const uint8_t *slot, uint32_t (&w)[16]) const
+    // Read this lane's block j (0 <= j < BPS) of the stage in `slot` as 16 little-endian words.
+    BRB_DEV void read(const uint8_t *slot, uint32_t j, uint32_t (&w)[16]) const
     {
-        const uint32_t sw = (lane >> 2) & 3;
+        const uint32_t f = swz(lane);
+        const uint8_t *row = slot + lane * S;
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(slot + lane_row + ((c ^ sw) << 4));
+            const uint32_t k = 4 * j + c;
+            const uint4 v = *reinterpret_cast<const uint4 *>(row + ((k ^ f) << 4));
             w[4 * c + 0] = v.x;
             w[4 * c + 1] = v.y;
             w[4 * c + 2] = v.z;

@@ -12,17 +12,7 @@
 #define BRB_MD5_F2(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
 #define BRB_MD5_F3(x, y, z) ((x) ^ (y) ^ (z))
 #define BRB_MD5_F4(x, y, z) ((y) ^ ((x) | ~(z)))
-// m + K as one VOP2 add with K as a literal operand: keeps the 64 round constants out of SGPRs
-// (hipcc otherwise parks them in SGPRs for v_add3, and the persistent DMA kernel then spills SGPRs
-// to VGPR lanes).  Not volatile: the scheduler is free to hoist it off the dependency chain.
-template <uint32_t K>
-BRB_DEV uint32_t add_k(uint32_t m)
-{
-    uint32_t r;
-    asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "i"(K), "v"(m));
-    return r;
-}
-#define BRB_MD5_STEP(F, a, b, c, d, m, k, s) (a) = (b) + rotl<s>((a) + F((b), (c), (d)) + add_k<k>(m))
+#define BRB_MD5_STEP(F, a, b, c, d, m, k, s) (a) = (b) + rotl<s>((a) + F((b), (c), (d)) + ((m) + (k)))
 
 struct Md5State {
     uint32_t a, b, c, d;

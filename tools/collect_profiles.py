@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Copy the rocprofv3 evidence of one GPU pass (tools/gpu_round.sh) into profiles/ and derive
+profiles/pmc_traffic.json, the per-launch HBM traffic bench.py reports as roofline.traffic.
+
+Traffic = (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 bytes per dispatch, mean over the profiled
+dispatches.  FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM: on gfx950 it reports half the
+bytes of a 16-B-per-lane streaming read, global_load and buffer_load ... lds alike (our staging is
+buffer_load_dwordx4 ... lds); WRITE_SIZE is exact for 16-B-per-lane stores (MD5 digests; the
+SHA-1 digests are 4-byte stores, WRITE_SIZE taken as reported).
+
+Usage: python tools/collect_profiles.py gpurun_out/r01 r01
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc_means(d, pat):
+    acc = {}
+    for p in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+        for row in csv.DictReader(open(p)):
+            if pat in row["Kernel_Name"]:
+                acc.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    for sub, name in (("prof", "bench_cfg2_md5"), ("prof4", "bench_cfg4_blowfish")):
+        f = os.path.join(src, sub, "run_kernel_stats.csv")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(prof, f"{tag}_{name}_kernel_stats.csv"))
+    traffic = {}
+    for sub, key, pat in (("pmc2", "cfg2_md5", "Md5Alg"), ("pmc2s", "cfg2_sha1", "Sha1Alg"), ("pmc4", "cfg4_blowfish", "bf_ecb")):
+        d = os.path.join(src, sub)
+        if not os.path.isdir(d):
+            continue
+        summ = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), d, pat],
+                              capture_output=True, text=True).stdout
+        with open(os.path.join(prof, f"{tag}_pmc_{key}.txt"), "w") as f:
+            f.write(f"# rocprofv3 --pmc passes (tools/gpu_pmc.sh), kernel filter '{pat}', mean per dispatch\n")
+            f.write(summ)
+        m = pmc_means(d, pat)
+        if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+            fetch = m["FETCH_SIZE"] * 2 * 1024
+            write = m["WRITE_SIZE"] * 1024
+            traffic[key] = int(fetch + write)
+            traffic[key + "_detail"] = {"fetch_bytes": int(fetch), "write_bytes": int(write),
+                                        "source": f"profiles/{tag}_pmc_{key}.txt",
+                                        "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024 per dispatch"}
+    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+        f.write("\n")
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()

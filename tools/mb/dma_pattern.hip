@@ -111,7 +111,7 @@ using Kern = void (*)(const uint8_t *, uint32_t, uint64_t, uint32_t *);
 int main(int argc, char **argv)
 {
     const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 1048576;
-    const uint32_t L = 1536;   // 24 blocks: divisible by BPS 1, 2, 4
+    const uint32_t L = argc > 2 ? atoi(argv[2]) : 1536;   // stages = floor(L / S)
     const int nrot = std::max<int>(2, int(700e6 / double(n * L)) + 1);
     std::vector<uint8_t *> d(nrot);
     for (int i = 0; i < nrot; i++) { CK(hipMalloc(&d[i], n * L + 8192)); CK(hipMemset(d[i], i + 1, n * L)); }

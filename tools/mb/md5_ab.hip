@@ -102,15 +102,17 @@ int main(int argc, char **argv)
     CK(hipMalloc(&o, n * 16));
     struct V { const char *name; Kern k; int waves; int cap; };
     std::vector<V> vs = {
-        {"persistent P3 lit-K", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 3, true>, 4, 768},
-        {"persistent P3 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, true>, 4, 768},
-        {"persistent P3 sched", brb_digest::digest_fixed_dma_kernel<AlgSched, 4, 3, true>, 4, 768},
-        {"persistent P2 lit-K", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, true>, 4, 1280},
-        {"persistent P2 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, true>, 4, 1280},
-        {"persistent P4 sgpr-K", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 4, true>, 4, 512},
-        {"DMA only P3 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, true>, 4, 768},
-        {"DMA only P4 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 4, true>, 4, 512},
-        {"DMA only P2 (memory floor)", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, true>, 4, 1280},
+        {"BPS2 P3 (product)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 2, true>, 4, 256},
+        {"BPS2 P2", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 2, true>, 4, 512},
+        {"BPS1 P3", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 1, true>, 4, 768},
+        {"BPS1 P4", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 4, 1, true>, 4, 512},
+        {"BPS1 P2 (5 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 1, true>, 4, 1280},
+        {"BPS1 P2 (2 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 1, true>, 4, 512},
+        {"BPS1 P3 (3 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 1, true>, 4, 768},
+        {"BPS2 P3 sched", brb_digest::digest_fixed_dma_kernel<AlgSched, 4, 3, 2, true>, 4, 256},
+        {"DMA only BPS2 P3", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, 2, true>, 4, 256},
+        {"DMA only BPS2 P2", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 2, true>, 4, 512},
+        {"DMA only BPS1 P3", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, 1, true>, 4, 768},
     };
     std::vector<uint8_t> ref(n * 16), got(n * 16);
     hipEvent_t e0, e1;
