@@ -29,6 +29,9 @@ extern "C" {
 /* ============================================================================================ */
 /* 1. COMPAT SURFACE                                                                              */
 /* ============================================================================================ */
+/* A translation unit that already includes the reference's libbrb_data.h (guard LIBBRB_DATA_H_)
+ * gets these types and prototypes from there; the definitions below are the same ABI. */
+#ifndef LIBBRB_DATA_H_
 
 /* ---- MD5 -- replaces libbrb_core/crypto/md5.c; prototypes libbrb_data.h:862-869 ------------ */
 #define MD5_DIGEST_LENGTH 16                      /* libbrb_data.h:852 */
@@ -78,6 +81,7 @@ typedef struct _BRB_BLOWFISH_CTX {                /* libbrb_data.h:876-879, size
 void BRB_Blowfish_Init(BRB_BLOWFISH_CTX *ctx, unsigned char *key, int keyLen);         /* :382 */
 void BRB_Blowfish_Encrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :312 */
 void BRB_Blowfish_Decrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :347 */
+#endif /* LIBBRB_DATA_H_ */
 
 /* ============================================================================================ */
 /* 2. BATCH SURFACE (GPU)                                                                         */
