@@ -39,7 +39,7 @@ def main():
         if os.path.exists(f):
             shutil.copy(f, os.path.join(prof, f"{tag}_{name}_kernel_stats.csv"))
     traffic = {}
-    for sub, key, pat in (("pmc2", "cfg2_md5", "Md5Alg"), ("pmc2s", "cfg2_sha1", "Sha1Alg"), ("pmc4", "cfg4_blowfish", "bf_ecb")):
+    for sub, key, pat in (("pmc2", "cfg2_md5", "Md5Alg"), ("pmc2s", "cfg2_sha1", "Sha1Alg"), ("pmc4", "cfg4_blowfish", "bf_rep_kernel")):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):
             continue
