@@ -1,4 +1,5 @@
-"""brb_framework_amd -- MI355X-native libbrb_core/crypto (MD5, SHA-1, 64-bit-word Blowfish).
+"""brb_framework_amd -- MI355X-native libbrb_core/crypto (MD5, SHA-1, 64-bit-word Blowfish, RC4 and
+the RC4+MD5 frame of the comm transform).
 
 The product is the C-ABI shared library ``libbrb_crypto_gpu.so`` built in this directory
 (``make -C brb_framework_amd``); its interface is ``include/brb_crypto.h``.  This Python package is
@@ -16,6 +17,9 @@ from .crypto import (  # noqa: F401
     BATCH_HOST,
     BRB_BLOWFISH_CTX,
     BRB_MD5_CTX,
+    BRB_RC4_State,
+    RC4_STATE_BYTES,
+    RC4MD5_HEADER,
     BrbSha1Ctx,
     LIB_PATH,
     blowfish_ctx_bytes,
@@ -27,6 +31,12 @@ from .crypto import (  # noqa: F401
     lib,
     md5_batch,
     md5_batch_fixed,
+    rc4_crypt_batch,
+    rc4_init,
+    rc4_state_bytes,
+    rc4_states,
+    rc4md5_frame_batch,
+    rc4md5_open_batch,
     sha1_batch,
     sha1_batch_fixed,
 )
@@ -35,5 +45,6 @@ __all__ = [
     "BATCH_ASYNC", "BATCH_DEVICE", "BATCH_HOST", "BRB_BLOWFISH_CTX", "BRB_MD5_CTX", "BrbSha1Ctx",
     "LIB_PATH", "blowfish_ctx_bytes", "blowfish_decrypt_batch", "blowfish_encrypt_batch",
     "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
-    "sha1_batch", "sha1_batch_fixed",
+    "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
+    "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch",
 ]

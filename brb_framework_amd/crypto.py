@@ -35,8 +35,20 @@ class BRB_BLOWFISH_CTX(ctypes.Structure):
     _fields_ = [("P", ctypes.c_ulong * 18), ("S", (ctypes.c_ulong * 256) * 4)]
 
 
+class _Rc4Flags(ctypes.Structure):
+    _fields_ = [("initialized", ctypes.c_uint, 1)]
+
+
+class BRB_RC4_State(ctypes.Structure):
+    """libbrb_data.h:887-897"""
+    _fields_ = [("perm", ctypes.c_ubyte * 256), ("index1", ctypes.c_ubyte), ("index2", ctypes.c_ubyte),
+                ("flags", _Rc4Flags)]
+
+
 assert ctypes.sizeof(BRB_MD5_CTX) == 168 and ctypes.sizeof(BrbSha1Ctx) == 92
-assert ctypes.sizeof(BRB_BLOWFISH_CTX) == 8336
+assert ctypes.sizeof(BRB_BLOWFISH_CTX) == 8336 and ctypes.sizeof(BRB_RC4_State) == 264
+RC4_STATE_BYTES = 264
+RC4MD5_HEADER = 30
 
 _LIB = None
 
@@ -58,6 +70,8 @@ _SIGNATURES = [
     ("BRB_Blowfish_Init", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ctypes.c_void_p, ctypes.c_int]),
     ("BRB_Blowfish_Encrypt", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ulp, ulp]),
     ("BRB_Blowfish_Decrypt", None, [ctypes.POINTER(BRB_BLOWFISH_CTX), ulp, ulp]),
+    ("BRB_RC4_Init", None, [ctypes.POINTER(BRB_RC4_State), ctypes.c_void_p, ctypes.c_int]),
+    ("BRB_RC4_Crypt", None, [ctypes.POINTER(BRB_RC4_State), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     ("BRB_MD5BatchFixed", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
     ("BRB_MD5Batch", ctypes.c_int,
@@ -72,6 +86,15 @@ _SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]),
     ("BRB_Blowfish_DecryptBatch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_RC4_CryptBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+      ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_RC4MD5_FrameBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_RC4MD5_OpenBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+      ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
@@ -236,3 +259,64 @@ def blowfish_encrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False)
 
 def blowfish_decrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False):
     return _bf(lib().BRB_Blowfish_DecryptBatch, ctx, words, n_blocks, stream, async_)
+
+
+# ---- RC4 and the RC4+MD5 frame ---------------------------------------------------
+def rc4_init(key: bytes, keylen: int | None = None) -> BRB_RC4_State:
+    """BRB_RC4_Init into a zeroed state."""
+    st = BRB_RC4_State()
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    lib().BRB_RC4_Init(ctypes.byref(st), kb, len(key) if keylen is None else keylen)
+    return st
+
+
+def rc4_state_bytes(st: BRB_RC4_State) -> bytes:
+    return ctypes.string_at(ctypes.addressof(st), RC4_STATE_BYTES)
+
+
+def rc4_states(keys) -> np.ndarray:
+    """(n, 264) uint8 array of BRB_RC4_Init states, one per key (the batch calls' `states`)."""
+    out = np.empty((len(keys), RC4_STATE_BYTES), np.uint8)
+    for i, k in enumerate(keys):
+        out[i] = np.frombuffer(rc4_state_bytes(rc4_init(k)), np.uint8)
+    return out
+
+
+def _same_kind(ref, *xs):
+    for x in xs:
+        if x is not None and _is_torch(x) != _is_torch(ref):
+            raise ValueError("all buffers of one batch call must be numpy (host) or all CUDA tensors (device)")
+
+
+def rc4_crypt_batch(states, data, offsets, lengths, out=None, stream=None, async_=False):
+    """BRB_RC4_CryptBatch: stream i = data[offsets[i]:+lengths[i]] -> out (in place when out is None).
+    states: (n, 264) uint8, updated in place."""
+    out = data if out is None else out
+    _same_kind(data, states, out, offsets, lengths)
+    flags, h = _mode(data, stream, async_)
+    _check(lib().BRB_RC4_CryptBatch(_ptr(states), _ptr(data), _ptr(out), _ptr(offsets), _ptr(lengths), len(offsets),
+                                    flags, h), "BRB_RC4_CryptBatch")
+    return out
+
+
+def rc4md5_frame_batch(states, payload, offsets, lengths, salts, frames, frame_offsets, stream=None, async_=False):
+    """BRB_RC4MD5_FrameBatch: frames[frame_offsets[i]:+30+lengths[i]] = RC4(salt|"HASH:"|MD5|NUL|payload)."""
+    _same_kind(payload, states, offsets, lengths, salts, frames, frame_offsets)
+    flags, h = _mode(payload, stream, async_)
+    _check(lib().BRB_RC4MD5_FrameBatch(_ptr(states), _ptr(payload), _ptr(offsets), _ptr(lengths), _ptr(salts),
+                                       _ptr(frames), _ptr(frame_offsets), len(offsets), flags, h),
+           "BRB_RC4MD5_FrameBatch")
+    return frames
+
+
+def rc4md5_open_batch(states, frames, offsets, lengths, out=None, valid=None, stream=None, async_=False):
+    """BRB_RC4MD5_OpenBatch: decrypt frames (in place when out is None); returns (out, valid uint8[n])."""
+    out = frames if out is None else out
+    n = len(offsets)
+    if valid is None:
+        valid = _out_like(frames, n, 1).reshape(n)
+    _same_kind(frames, states, out, offsets, lengths, valid)
+    flags, h = _mode(frames, stream, async_)
+    _check(lib().BRB_RC4MD5_OpenBatch(_ptr(states), _ptr(frames), _ptr(out), _ptr(offsets), _ptr(lengths), n,
+                                      _ptr(valid), flags, h), "BRB_RC4MD5_OpenBatch")
+    return out, valid

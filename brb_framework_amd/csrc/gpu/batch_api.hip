@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "brb_crypto.h"
 #include "brb_kernels.h"
@@ -243,6 +244,205 @@ int blowfish_batch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n
     return finish(s, flags & ~BRB_BATCH_ASYNC);
 }
 
+// ---- host-mode staging for the multi-buffer (RC4) batches --------------------------------------
+// Segments are laid out back to back (256-B aligned) in the per-thread workspace; `in` segments are
+// copied H2D before the launch, `out` segments D2H after it (a segment may be both).
+struct Staging {
+    struct Seg {
+        const void *h_in;
+        void *h_out;
+        size_t bytes, off;
+    };
+    std::vector<Seg> segs;
+    size_t total = 0;
+    uint8_t *ws = nullptr;
+
+    size_t add(const void *h_in, void *h_out, size_t bytes)
+    {
+        segs.push_back({h_in, h_out, bytes, total});
+        total = align_up(total + bytes, 256);
+        return segs.size() - 1;
+    }
+    uint8_t *dev(size_t i) const { return ws + segs[i].off; }
+
+    int upload(hipStream_t s)
+    {
+        hipError_t e;
+        ws = static_cast<uint8_t *>(workspace(std::max<size_t>(total, 256), &e));
+        if (!ws)
+            return fail_hip("device workspace", e);
+        for (const Seg &g : segs)
+            if (g.h_in && g.bytes && (e = hipMemcpyAsync(ws + g.off, g.h_in, g.bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+                return fail_hip("hipMemcpyAsync H2D", e);
+        return BRB_BATCH_OK;
+    }
+    int download(hipStream_t s)
+    {
+        hipError_t e;
+        for (const Seg &g : segs)
+            if (g.h_out && g.bytes && (e = hipMemcpyAsync(g.h_out, ws + g.off, g.bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
+                return fail_hip("hipMemcpyAsync D2H", e);
+        return finish(s, 0);
+    }
+};
+
+// [lo, hi) covered by ranges offsets[i] .. + lengths[i] + extra (empty ranges ignored)
+void span_of(const uint64_t *offs, const uint32_t *lens, uint64_t n, uint64_t extra, uint64_t &lo, uint64_t &hi)
+{
+    lo = UINT64_MAX;
+    hi = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t len = uint64_t(lens[i]) + extra;
+        if (!len)
+            continue;
+        lo = std::min(lo, offs[i]);
+        hi = std::max(hi, offs[i] + len);
+    }
+    if (lo == UINT64_MAX)
+        lo = hi = 0;
+}
+
+std::vector<uint64_t> rebase(const uint64_t *offs, uint64_t n, uint64_t lo)
+{
+    std::vector<uint64_t> r(n);
+    for (uint64_t i = 0; i < n; i++)
+        r[i] = offs[i] >= lo ? offs[i] - lo : 0;
+    return r;
+}
+
+int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint64_t *offsets, const uint32_t *lengths,
+                    uint64_t n, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n == 0)
+        return BRB_BATCH_OK;
+    if (!states || !in || !out || !offsets || !lengths) {
+        set_err("NULL states, in, out, offsets or lengths");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = brb::launch_rc4_crypt(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(in),
+                                  static_cast<uint8_t *>(out), offsets, lengths, n, s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    uint64_t lo, hi;
+    span_of(offsets, lengths, n, 0, lo, hi);
+    const std::vector<uint64_t> roff = rebase(offsets, n, lo);
+    const size_t span = size_t(hi - lo);
+    Staging st;
+    const size_t i_st = st.add(states, states, sizeof(BRB_RC4_State) * n);
+    const size_t i_in = st.add(static_cast<const uint8_t *>(in) + lo, in == out ? static_cast<uint8_t *>(out) + lo : nullptr, span);
+    // a separate output buffer is staged with its current bytes so that bytes outside the streams survive
+    const size_t i_out = in == out ? i_in : st.add(static_cast<uint8_t *>(out) + lo, static_cast<uint8_t *>(out) + lo, span);
+    const size_t i_off = st.add(roff.data(), nullptr, 8 * n);
+    const size_t i_len = st.add(lengths, nullptr, 4 * n);
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_rc4_crypt(st.dev(i_st), st.dev(i_in), st.dev(i_out), reinterpret_cast<const uint64_t *>(st.dev(i_off)),
+                                   reinterpret_cast<const uint32_t *>(st.dev(i_len)), n, s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
+int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_t *offsets, const uint32_t *lengths,
+                       const uint64_t *salts, void *frames, const uint64_t *frame_offsets, uint64_t n, unsigned flags,
+                       void *stream)
+{
+    t_err.clear();
+    if (n == 0)
+        return BRB_BATCH_OK;
+    if (!states || !payload || !offsets || !lengths || !salts || !frames || !frame_offsets) {
+        set_err("NULL states, payload, offsets, lengths, salts, frames or frame_offsets");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = brb::launch_rc4md5_frame(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(payload), offsets,
+                                     lengths, salts, static_cast<uint8_t *>(frames), frame_offsets, n, s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    uint64_t plo, phi, flo, fhi;
+    span_of(offsets, lengths, n, 0, plo, phi);
+    span_of(frame_offsets, lengths, n, BRB_RC4MD5_HEADER, flo, fhi);
+    const std::vector<uint64_t> poff = rebase(offsets, n, plo), foff = rebase(frame_offsets, n, flo);
+    Staging st;
+    const size_t i_st = st.add(states, states, sizeof(BRB_RC4_State) * n);
+    const size_t i_pl = st.add(static_cast<const uint8_t *>(payload) + plo, nullptr, size_t(phi - plo));
+    const size_t i_fr = st.add(static_cast<uint8_t *>(frames) + flo, static_cast<uint8_t *>(frames) + flo, size_t(fhi - flo));
+    const size_t i_po = st.add(poff.data(), nullptr, 8 * n);
+    const size_t i_fo = st.add(foff.data(), nullptr, 8 * n);
+    const size_t i_len = st.add(lengths, nullptr, 4 * n);
+    const size_t i_salt = st.add(salts, nullptr, 8 * n);
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_rc4md5_frame(st.dev(i_st), st.dev(i_pl), reinterpret_cast<const uint64_t *>(st.dev(i_po)),
+                                      reinterpret_cast<const uint32_t *>(st.dev(i_len)),
+                                      reinterpret_cast<const uint64_t *>(st.dev(i_salt)), st.dev(i_fr),
+                                      reinterpret_cast<const uint64_t *>(st.dev(i_fo)), n, s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
+int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, const uint64_t *offsets,
+                      const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n == 0)
+        return BRB_BATCH_OK;
+    if (!states || !frames || !out || !offsets || !lengths || !valid) {
+        set_err("NULL states, frames, out, offsets, lengths or valid");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = brb::launch_rc4md5_open(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(frames),
+                                    static_cast<uint8_t *>(out), offsets, lengths, n, valid, s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    uint64_t lo, hi;
+    span_of(offsets, lengths, n, 0, lo, hi);
+    const std::vector<uint64_t> roff = rebase(offsets, n, lo);
+    const size_t span = size_t(hi - lo);
+    Staging st;
+    const size_t i_st = st.add(states, states, sizeof(BRB_RC4_State) * n);
+    const size_t i_in = st.add(static_cast<const uint8_t *>(frames) + lo, frames == out ? static_cast<uint8_t *>(out) + lo : nullptr, span);
+    const size_t i_out = frames == out ? i_in : st.add(static_cast<uint8_t *>(out) + lo, static_cast<uint8_t *>(out) + lo, span);
+    const size_t i_off = st.add(roff.data(), nullptr, 8 * n);
+    const size_t i_len = st.add(lengths, nullptr, 4 * n);
+    const size_t i_val = st.add(nullptr, valid, n);
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_rc4md5_open(st.dev(i_st), st.dev(i_in), st.dev(i_out), reinterpret_cast<const uint64_t *>(st.dev(i_off)),
+                                     reinterpret_cast<const uint32_t *>(st.dev(i_len)), n, st.dev(i_val), s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -281,6 +481,25 @@ int BRB_Blowfish_DecryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words,
                               void *hip_stream)
 {
     return blowfish_batch(ctx, words, n_blocks, flags, hip_stream, true);
+}
+
+int BRB_RC4_CryptBatch(BRB_RC4_State *states, const void *in, void *out, const uint64_t *offsets, const uint32_t *lengths,
+                       uint64_t n_streams, unsigned flags, void *hip_stream)
+{
+    return rc4_crypt_batch(states, in, out, offsets, lengths, n_streams, flags, hip_stream);
+}
+
+int BRB_RC4MD5_FrameBatch(BRB_RC4_State *states, const void *payload, const uint64_t *offsets, const uint32_t *lengths,
+                          const uint64_t *salts, void *frames, const uint64_t *frame_offsets, uint64_t n, unsigned flags,
+                          void *hip_stream)
+{
+    return rc4md5_frame_batch(states, payload, offsets, lengths, salts, frames, frame_offsets, n, flags, hip_stream);
+}
+
+int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, const uint64_t *offsets,
+                         const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags, void *hip_stream)
+{
+    return rc4md5_open_batch(states, frames, out, offsets, lengths, n, valid, flags, hip_stream);
 }
 
 int BRB_CryptoGPU_Available(void)

@@ -18,4 +18,13 @@ hipError_t launch_sha1_var(const uint8_t *data, const uint64_t *offs, const uint
 // ctx_dev: device copy of BRB_BLOWFISH_CTX (P[18] then S[4][256], 64-bit words)
 hipError_t launch_blowfish(const uint64_t *ctx_dev, uint64_t *words, uint64_t n_blocks, bool decrypt, hipStream_t s);
 
+// RC4 (rc4_kernels.hip): states = n contiguous 264-byte BRB_RC4_State, updated in place
+hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
+                            const uint32_t *lens, uint64_t n, hipStream_t s);
+hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const uint64_t *offs, const uint32_t *lens,
+                               const uint64_t *salts, uint8_t *frames, const uint64_t *foffs, uint64_t n,
+                               hipStream_t s);
+hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
+                              const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s);
+
 }  // namespace brb

@@ -81,6 +81,20 @@ typedef struct _BRB_BLOWFISH_CTX {                /* libbrb_data.h:876-879, size
 void BRB_Blowfish_Init(BRB_BLOWFISH_CTX *ctx, unsigned char *key, int keyLen);         /* :382 */
 void BRB_Blowfish_Encrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :312 */
 void BRB_Blowfish_Decrypt(BRB_BLOWFISH_CTX *ctx, unsigned long *xl, unsigned long *xr); /* :347 */
+
+/* ---- RC4 -- replaces libbrb_core/crypto/rc4.c; prototypes libbrb_data.h:899-900 ------------ */
+typedef struct _BRB_RC4_State {                   /* libbrb_data.h:887-897, sizeof == 264 */
+    unsigned char perm[256];
+    unsigned char index1;
+    unsigned char index2;
+    struct {
+        unsigned int initialized : 1;
+    } flags;
+} BRB_RC4_State;
+
+void BRB_RC4_Init(BRB_RC4_State *state, const unsigned char *key, int keylen);            /* rc4.c:40 */
+void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned char *outbuf,
+                   int buflen);                                                          /* rc4.c:64 */
 #endif /* LIBBRB_DATA_H_ */
 
 /* ============================================================================================ */
@@ -132,6 +146,38 @@ int BRB_Blowfish_EncryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words,
                               unsigned flags, void *hip_stream);
 int BRB_Blowfish_DecryptBatch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n_blocks,
                               unsigned flags, void *hip_stream);
+
+/* ---- RC4 and the RC4+MD5 frame of the comm transform -------------------------
+ * One stream per connection; states[i] is that connection's BRB_RC4_State (an array of n
+ * contiguous 264-byte states) and advances exactly as the scalar calls would.  Streams of one
+ * call must belong to different connections (a connection's buffers are sequential). */
+
+/* out[offsets[i] .. + lengths[i]) = BRB_RC4_Crypt(&states[i], in + offsets[i], ..., lengths[i]).
+ * out may equal in (in place); otherwise the ranges of in and out must not overlap. */
+int BRB_RC4_CryptBatch(BRB_RC4_State *states, const void *in, void *out, const uint64_t *offsets,
+                       const uint32_t *lengths, uint64_t n_streams, unsigned flags, void *hip_stream);
+
+/* Bytes before the payload in a frame: salt (8) "HASH:" (5) MD5 (16) NUL (1). */
+#define BRB_RC4MD5_HEADER 30
+
+/* WRITE side of EvAIOReqTransform_CryptoRaw(COMM_CRYPTO_FUNC_RC4_MD5) (ev_kq_aio_transform.c:
+ * 212-230, 281-283) for n connections: with payload i = payload[offsets[i] .. + lengths[i]),
+ *   frames[frame_offsets[i] .. + 30 + lengths[i]) =
+ *       RC4(states[i], salts[i] as 8 LE bytes | "HASH:" | MD5(payload i) | NUL | payload i).
+ * salts[i] is the caller's arc4random() value (the reference's `unsigned long random_salt`).
+ * The frames must not overlap each other or the payloads. */
+int BRB_RC4MD5_FrameBatch(BRB_RC4_State *states, const void *payload, const uint64_t *offsets,
+                          const uint32_t *lengths, const uint64_t *salts, void *frames,
+                          const uint64_t *frame_offsets, uint64_t n, unsigned flags, void *hip_stream);
+
+/* READ side (ev_kq_aio_transform.c:270-279) followed by EvAIOReqTransform_RC4_MD5_DataValidate
+ * (:158-184): frame i = frames[offsets[i] .. + lengths[i]) is RC4-decrypted with states[i] into
+ * out at the same offset (out may equal frames), and valid[i] = 1 if bytes 8..12 are "HASH:" and
+ * bytes 13..28 are the MD5 of bytes 30.., else 0.  A frame shorter than 30 bytes is decrypted and
+ * reported invalid (the reference would digest past the end of the buffer). */
+int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, const uint64_t *offsets,
+                         const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags,
+                         void *hip_stream);
 
 /* ---- runtime ---------------------------------------------------------------------------- */
 /* 1 if a HIP device is usable from this process, else 0 (reason in LastError). */

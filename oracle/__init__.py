@@ -45,6 +45,10 @@ def lib() -> ctypes.CDLL:
             "orc_sha1_batch_fixed": (None, [vp, ctypes.c_uint32, u64, vp, ctypes.c_int]),
             "orc_md5_batch": (None, [vp, vp, vp, u64, vp]),
             "orc_sha1_batch": (None, [vp, vp, vp, u64, vp]),
+            "orc_rc4_init": (None, [vp, vp, ctypes.c_int]),
+            "orc_rc4_crypt": (None, [vp, vp, vp, ctypes.c_int]),
+            "orc_rc4md5_frame": (None, [vp, vp, u64, u64, vp]),
+            "orc_rc4md5_open": (ctypes.c_int, [vp, vp, u64]),
             "orc_splitmix64": (u64, [u64]),
             "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
         }
@@ -160,6 +164,43 @@ def membuf_key(seed: int) -> bytes:
     k = (ctypes.c_uint * 16)()
     lib().orc_membuf_key(seed, k)
     return bytes(k)
+
+
+# ---- RC4 and RC4+MD5 framing ------------------------------------------------------------------
+RC4_STATE_BYTES = 264      # sizeof(BRB_RC4_State), libbrb_data.h:887-897
+RC4MD5_HDR = 30            # salt(8) "HASH:"(5) md5(16) NUL(1)
+
+
+def rc4_init(key: bytes, keylen: int | None = None) -> bytes:
+    """BRB_RC4_Init (rc4.c:40-62) into a zeroed 264-byte state; returns the state bytes."""
+    st = ctypes.create_string_buffer(RC4_STATE_BYTES)
+    kb = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    lib().orc_rc4_init(st, kb, len(key) if keylen is None else keylen)
+    return st.raw
+
+
+def rc4_crypt(state: bytes, data: bytes) -> tuple[bytes, bytes]:
+    """BRB_RC4_Crypt (rc4.c:64-87): returns (new state bytes, output bytes)."""
+    st = ctypes.create_string_buffer(bytes(state), RC4_STATE_BYTES)
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    lib().orc_rc4_crypt(st, bytes(data), out, len(data))
+    return st.raw, out.raw[: len(data)]
+
+
+def rc4md5_frame(state: bytes, payload: bytes, salt: int) -> tuple[bytes, bytes]:
+    """WRITE side of EvAIOReqTransform_CryptoRaw (ev_kq_aio_transform.c:212-230, :281-283)."""
+    st = ctypes.create_string_buffer(bytes(state), RC4_STATE_BYTES)
+    fr = ctypes.create_string_buffer(RC4MD5_HDR + len(payload))
+    lib().orc_rc4md5_frame(st, bytes(payload), len(payload), salt, fr)
+    return st.raw, fr.raw
+
+
+def rc4md5_open(state: bytes, frame: bytes) -> tuple[bytes, bytes, int]:
+    """READ side (:270-279) + DataValidate (:158-184): returns (new state, decrypted frame, valid)."""
+    st = ctypes.create_string_buffer(bytes(state), RC4_STATE_BYTES)
+    fr = ctypes.create_string_buffer(bytes(frame), max(len(frame), 1))
+    ok = lib().orc_rc4md5_open(st, fr, len(frame))
+    return st.raw, fr.raw[: len(frame)], ok
 
 
 # ---- generator (SURVEY.md §8(d)) ---------------------------------------------------------------

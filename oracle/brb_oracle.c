@@ -494,6 +494,79 @@ void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *le
 }
 
 /* =========================================================================================== */
+/* RC4 -- libbrb_core/crypto/rc4.c                                                               */
+/* =========================================================================================== */
+
+/* rc4.c:40-62: identity permutation, indices zeroed, then one key-scheduling sweep with an 8-bit
+ * accumulator j and key bytes cycled by i % keylen.  `flags` is left as it was. */
+void orc_rc4_init(orc_rc4_state *s, const unsigned char *key, int keylen)
+{
+    for (int i = 0; i < 256; i++) s->perm[i] = (unsigned char)i;
+    s->index1 = 0;
+    s->index2 = 0;
+    unsigned j = 0;
+    for (int i = 0; i < 256; i++) {
+        j = (j + s->perm[i] + key[i % keylen]) & 255u;
+        unsigned char t = s->perm[i];
+        s->perm[i] = s->perm[j];
+        s->perm[j] = t;
+    }
+}
+
+/* rc4.c:64-87: per byte, index1 += 1, index2 += perm[index1], swap, out = in ^ perm[perm[index1] +
+ * perm[index2]] (all 8-bit).  in == out is allowed. */
+void orc_rc4_crypt(orc_rc4_state *s, const unsigned char *in, unsigned char *out, int n)
+{
+    unsigned a = s->index1, b = s->index2;
+    for (int k = 0; k < n; k++) {
+        a = (a + 1) & 255u;
+        b = (b + s->perm[a]) & 255u;
+        unsigned char t = s->perm[a];
+        s->perm[a] = s->perm[b];
+        s->perm[b] = t;
+        out[k] = in[k] ^ s->perm[(s->perm[a] + s->perm[b]) & 255u];
+    }
+    s->index1 = (unsigned char)a;
+    s->index2 = (unsigned char)b;
+}
+
+/* RC4 over more than INT_MAX bytes in int-sized pieces (the keystream is position-only). */
+static void rc4_crypt_big(orc_rc4_state *s, const uint8_t *in, uint8_t *out, uint64_t n)
+{
+    while (n) {
+        int piece = n > (1u << 30) ? (1 << 30) : (int)n;
+        orc_rc4_crypt(s, in, out, piece);
+        in += piece;
+        out += piece;
+        n -= (uint64_t)piece;
+    }
+}
+
+/* ev_kq_aio_transform.c:212-230 then :281-283 (WRITE side). */
+void orc_rc4md5_frame(orc_rc4_state *s, const uint8_t *payload, uint64_t len, uint64_t salt, uint8_t *frame)
+{
+    uint8_t dig[16];
+    orc_md5(payload, len, dig);
+    memcpy(frame, &salt, 8);                /* MemBufferAdd(&random_salt, sizeof(unsigned long)) */
+    memcpy(frame + 8, "HASH:", 5);
+    memcpy(frame + 13, dig, 16);
+    frame[29] = 0;
+    memcpy(frame + ORC_RC4MD5_HDR, payload, len);
+    rc4_crypt_big(s, frame, frame, ORC_RC4MD5_HDR + len);
+}
+
+/* ev_kq_aio_transform.c:270-279 (READ side, in place) then DataValidate (:158-184). */
+int orc_rc4md5_open(orc_rc4_state *s, uint8_t *frame, uint64_t frame_len)
+{
+    rc4_crypt_big(s, frame, frame, frame_len);
+    if (frame_len < ORC_RC4MD5_HDR) return 0;
+    if (memcmp(frame + 8, "HASH:", 5)) return 0;
+    uint8_t dig[16];
+    orc_md5(frame + ORC_RC4MD5_HDR, frame_len - ORC_RC4MD5_HDR, dig);
+    return memcmp(dig, frame + 13, 16) == 0;
+}
+
+/* =========================================================================================== */
 /* Generator                                                                                     */
 /* =========================================================================================== */
 uint64_t orc_splitmix64(uint64_t x)

@@ -81,6 +81,29 @@ void orc_membuf_key(unsigned int seed, unsigned int key_out[16]);
 uint64_t orc_membuf_encrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset);
 uint64_t orc_membuf_decrypt(uint8_t *buf, uint64_t size, unsigned int seed, uint64_t offset);
 
+/* ---- RC4 -- libbrb_core/crypto/rc4.c ------------------------------------------------------
+ * State layout = BRB_RC4_State (libbrb_data.h:887-897): perm[256], index1, index2, flags. */
+typedef struct {
+    unsigned char perm[256];
+    unsigned char index1;
+    unsigned char index2;
+    struct { unsigned int initialized : 1; } flags;
+} orc_rc4_state;
+
+void orc_rc4_init(orc_rc4_state *s, const unsigned char *key, int keylen);            /* rc4.c:40-62 */
+void orc_rc4_crypt(orc_rc4_state *s, const unsigned char *in, unsigned char *out, int n); /* rc4.c:64-87 */
+
+/* ---- RC4+MD5 framing -- EvAIOReqTransform_CryptoRaw, ev_kq_aio_transform.c:189-288 --------
+ * WRITE (:212-230, :281-283): frame = salt (8 B, LP64 unsigned long) | "HASH:" | MD5(payload) |
+ *   NUL | payload, then RC4 with the write state.  `frame` receives 30 + len bytes.
+ * READ (:232-236, :270-279): RC4 with the read state over the whole received buffer, in place.
+ * VALIDATE (EvAIOReqTransform_RC4_MD5_DataValidate, :158-184): "HASH:" at 8 and MD5 of bytes
+ *   [30, size) equal to bytes [13, 29).  Frames shorter than 30 B are reported invalid (the
+ *   reference would read past the frame and digest ~2^64 bytes: undefined). */
+#define ORC_RC4MD5_HDR 30
+void orc_rc4md5_frame(orc_rc4_state *s, const uint8_t *payload, uint64_t len, uint64_t salt, uint8_t *frame);
+int orc_rc4md5_open(orc_rc4_state *s, uint8_t *frame, uint64_t frame_len);
+
 /* ---- Batches (used by tests and by bench.py's cpu_baseline) ------------------------------- */
 void orc_md5_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out16, int n_threads);
 void orc_sha1_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out20, int n_threads);

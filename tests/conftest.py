@@ -17,7 +17,7 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     out = {}
-    for name in ("kat", "digests", "blowfish64", "quirks"):
+    for name in ("kat", "digests", "blowfish64", "quirks", "rc4"):
         with open(os.path.join(GOLDEN, name + ".json")) as f:
             out[name] = json.load(f)
     return out

@@ -74,6 +74,25 @@ def libcrypto_bf(key: bytes, pt: bytes) -> bytes:
     return out.raw
 
 
+RC4_KAT = [  # (key hex, plaintext hex, ciphertext hex): RFC 6229 section 2 (key 0x0102030405,
+    # keystream offset 0) and the three classic vectors ("Key"/"Wiki"/"Secret")
+    ("0102030405", "00" * 16, "b2396305f03dc027ccc3524a0a1118a8"),
+    (b"Key".hex(), b"Plaintext".hex(), "bbf316e8d940af0ad3"),
+    (b"Wiki".hex(), b"pedia".hex(), "1021bf0420"),
+    (b"Secret".hex(), b"Attack at dawn".hex(), "45a01f645fc35b383552544b9bf5"),
+]
+
+
+def libcrypto_rc4(key: bytes, data: bytes) -> bytes:
+    """OpenSSL's RC4 (RC4_set_key / RC4, libcrypto.so.3): an independent implementation."""
+    L = ctypes.CDLL("libcrypto.so.3")
+    ks = ctypes.create_string_buffer(2048)        # RC4_KEY = {uint x, y; uint data[256]}
+    L.RC4_set_key(ks, len(key), key)
+    out = ctypes.create_string_buffer(max(len(data), 1))
+    L.RC4(ks, ctypes.c_size_t(len(data)), data, out)
+    return out.raw[: len(data)]
+
+
 def dump(name, obj):
     with open(os.path.join(OUT, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -160,6 +179,41 @@ def main():
                          "hashlib_digest": hashlib.sha1(before).hexdigest()},
         "membuffer": mb,
         "membuf_key_4fd9": oracle.membuf_key(0x4FD9).hex(),
+    })
+    # ---- RC4 and the RC4+MD5 frame ----
+    for k, p_, c in RC4_KAT:
+        key, pt = bytes.fromhex(k), bytes.fromhex(p_)
+        assert libcrypto_rc4(key, pt).hex() == c, k
+        assert oracle.rc4_crypt(oracle.rc4_init(key), pt)[1].hex() == c, k
+    streams = []
+    for key, lens in ((b"cryptokey", (1, 2, 3, 64, 1000)), (bytes(range(1, 41)), (300, 5)), (b"\xff", (777,))):
+        st = oracle.rc4_init(key)
+        data = workload.gen_records(seed, 21, 1, sum(lens)).tobytes()
+        outs, pos = [], 0
+        for n in lens:            # the state carries across calls (one connection, several buffers)
+            st, o = oracle.rc4_crypt(st, data[pos:pos + n])
+            outs.append(o.hex())
+            pos += n
+        assert b"".join(bytes.fromhex(o) for o in outs) == libcrypto_rc4(key, data)
+        streams.append({"key": key.hex(), "lens": list(lens), "data": data.hex(), "out": outs, "state_after": st.hex()})
+    frames = []
+    for i, n in enumerate((0, 1, 2, 3, 26, 55, 56, 63, 64, 65, 100, 1500)):
+        key = b"cryptokey" if i % 2 == 0 else bytes([i + 1] * (i + 3))
+        st0 = oracle.rc4_init(key)
+        payload = workload.gen_records(seed, 40 + i, 1, n).tobytes() if n else b""
+        salt = (0x9E3779B9 * (i + 1)) & 0xFFFFFFFF      # arc4random(): upper 4 bytes zero on LP64
+        st_w, fr = oracle.rc4md5_frame(st0, payload, salt)
+        assert fr == libcrypto_rc4(key, salt.to_bytes(8, "little") + b"HASH:" + hashlib.md5(payload).digest() + b"\0" + payload)
+        st_r, dec, ok = oracle.rc4md5_open(st0, fr)
+        assert ok == 1 and dec[30:] == payload and st_r == st_w
+        frames.append({"key": key.hex(), "salt": salt, "payload": payload.hex(), "frame": fr.hex(),
+                       "state_after": st_w.hex()})
+    dump("rc4.json", {
+        "source": "published KATs (RFC 6229, classic vectors) and oracle frames, all re-checked against "
+                  "OpenSSL RC4 + hashlib MD5",
+        "kat": [{"key": k, "plain": p_, "cipher": c} for k, p_, c in RC4_KAT],
+        "streams": streams,
+        "frames": frames,
     })
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".json")))
 

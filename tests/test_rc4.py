@@ -1,0 +1,330 @@
+"""RC4 and the RC4+MD5 frame of the comm transform.
+
+CPU (not gpu): the oracle against the published RC4 vectors and OpenSSL, the compat BRB_RC4_* of
+the product library against the oracle, and the frame fixtures (tests/golden/rc4.json).
+GPU: BRB_RC4_CryptBatch / BRB_RC4MD5_FrameBatch / BRB_RC4MD5_OpenBatch through the C ABI against
+the oracle, bit for bit, on ragged, misaligned and back-to-back streams, in host and device mode.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+SEED = 0x5EED00F1
+
+
+def _libcrypto():
+    try:
+        return ctypes.CDLL("libcrypto.so.3")
+    except OSError:
+        return None
+
+
+# ---------------------------------------------------------------------------------------------
+# CPU: oracle and compat surface
+# ---------------------------------------------------------------------------------------------
+def test_oracle_rc4_kat(orc, golden):
+    for v in golden["rc4"]["kat"]:
+        st = orc.rc4_init(bytes.fromhex(v["key"]))
+        assert orc.rc4_crypt(st, bytes.fromhex(v["plain"]))[1].hex() == v["cipher"]
+
+
+def test_oracle_rc4_vs_openssl(orc):
+    L = _libcrypto()
+    if L is None:
+        pytest.skip("libcrypto.so.3 not present")
+    rng = np.random.default_rng(11)
+    for _ in range(30):
+        key = rng.integers(0, 256, int(rng.integers(1, 257)), dtype=np.uint8).tobytes()
+        data = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        ks = ctypes.create_string_buffer(2048)
+        L.RC4_set_key(ks, len(key), key)
+        out = ctypes.create_string_buffer(max(len(data), 1))
+        L.RC4(ks, ctypes.c_size_t(len(data)), data, out)
+        assert orc.rc4_crypt(orc.rc4_init(key), data)[1] == out.raw[: len(data)]
+
+
+def test_oracle_streams_carry_state(orc, golden):
+    for v in golden["rc4"]["streams"]:
+        st = orc.rc4_init(bytes.fromhex(v["key"]))
+        data, pos = bytes.fromhex(v["data"]), 0
+        for n, want in zip(v["lens"], v["out"]):
+            st, o = orc.rc4_crypt(st, data[pos:pos + n])
+            assert o.hex() == want
+            pos += n
+        assert st.hex() == v["state_after"]
+
+
+def test_oracle_frames(orc, golden):
+    for v in golden["rc4"]["frames"]:
+        st0 = orc.rc4_init(bytes.fromhex(v["key"]))
+        payload = bytes.fromhex(v["payload"])
+        st_w, fr = orc.rc4md5_frame(st0, payload, v["salt"])
+        assert fr.hex() == v["frame"] and st_w.hex() == v["state_after"]
+        st_r, dec, ok = orc.rc4md5_open(st0, fr)
+        assert ok == 1 and dec[30:] == payload and dec[8:13] == b"HASH:"
+        assert dec[13:29] == hashlib.md5(payload).digest() and dec[29] == 0
+        assert int.from_bytes(dec[:8], "little") == v["salt"]
+
+
+def test_oracle_open_rejects(orc):
+    st0 = orc.rc4_init(b"cryptokey")
+    _, fr = orc.rc4md5_frame(st0, b"payload bytes", 7)
+    for pos in (8, 12, 13, 28, 30, len(fr) - 1):
+        bad = bytearray(fr)
+        bad[pos] ^= 1
+        assert orc.rc4md5_open(st0, bytes(bad))[2] == 0, pos
+    for pos in (0, 7, 29):       # salt and NUL are not checked (ev_kq_aio_transform.c:167-181)
+        bad = bytearray(fr)
+        bad[pos] ^= 1
+        assert orc.rc4md5_open(st0, bytes(bad))[2] == 1, pos
+    assert orc.rc4md5_open(st0, fr[:29])[2] == 0
+
+
+def test_compat_rc4_matches_oracle(brb, orc, golden):
+    for v in golden["rc4"]["kat"]:
+        key, pt = bytes.fromhex(v["key"]), bytes.fromhex(v["plain"])
+        st = brb.rc4_init(key)
+        assert brb.rc4_state_bytes(st) == orc.rc4_init(key)
+        out = ctypes.create_string_buffer(len(pt))
+        brb.lib().BRB_RC4_Crypt(ctypes.byref(st), pt, out, len(pt))
+        assert out.raw.hex() == v["cipher"]
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        key = rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tobytes()
+        st, ost = brb.rc4_init(key), orc.rc4_init(key)
+        for _ in range(3):          # the state carries across calls
+            data = rng.integers(0, 256, int(rng.integers(0, 700)), dtype=np.uint8).tobytes()
+            buf = ctypes.create_string_buffer(data, max(len(data), 1))
+            brb.lib().BRB_RC4_Crypt(ctypes.byref(st), buf, buf, len(data))     # in place
+            ost, want = orc.rc4_crypt(ost, data)
+            assert buf.raw[: len(data)] == want and brb.rc4_state_bytes(st) == ost
+
+
+def test_rc4_state_layout(brb):
+    st = brb.BRB_RC4_State()
+    assert ctypes.sizeof(st) == 264
+    assert brb.BRB_RC4_State.index1.offset == 256 and brb.BRB_RC4_State.index2.offset == 257
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU
+# ---------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def torch_dev(brb):
+    import torch
+    assert torch.cuda.is_available(), "no HIP device visible to torch"
+    assert brb.gpu_available(), brb.lib().BRB_CryptoGPU_LastError()
+    return torch
+
+
+def _keys(n, seed=1):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, int(rng.integers(1, 64)), dtype=np.uint8).tobytes() for _ in range(n)]
+
+
+def _layout(lens, gap_seed=None, base=0):
+    """Back-to-back stream offsets (optionally with random 0..5-byte gaps) starting at `base`."""
+    rng = np.random.default_rng(gap_seed) if gap_seed is not None else None
+    offs, pos = [], base
+    for n in lens:
+        if rng is not None:
+            pos += int(rng.integers(0, 6))
+        offs.append(pos)
+        pos += int(n)
+    return np.array(offs, np.uint64), np.array(lens, np.uint32), pos
+
+
+def _oracle_crypt(orc, states, data, offs, lens):
+    out = data.copy()
+    st = states.copy()
+    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+        s2, ob = orc.rc4_crypt(st[i].tobytes(), data[o:o + n].tobytes())
+        st[i] = np.frombuffer(s2, np.uint8)
+        out[o:o + n] = np.frombuffer(ob, np.uint8)
+    return st, out
+
+
+def _to(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+RAGGED = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 29, 30, 31, 32, 33, 63, 64, 65, 100, 255, 256, 257, 1000, 1500, 4099]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gaps", [None, 5])
+@pytest.mark.parametrize("base", [0, 1, 2, 3])
+def test_rc4_crypt_batch_ragged(brb, orc, torch_dev, gaps, base):
+    lens = (RAGGED * 5)[: 130]
+    offs, lens, total = _layout(lens, gaps, base)
+    data = workload.gen_records(SEED, base, 1, total + 8)
+    states = brb.rc4_states(_keys(len(offs)))
+    want_st, want = _oracle_crypt(orc, states, data, offs, lens)
+    # device mode, in place
+    t = _to(torch_dev, data)
+    ts = _to(torch_dev, states)
+    brb.rc4_crypt_batch(ts, t, _to(torch_dev, offs), _to(torch_dev, lens))
+    assert np.array_equal(t.cpu().numpy(), want)
+    assert np.array_equal(ts.cpu().numpy(), want_st)
+    # host mode, out of place: bytes outside the streams keep the output buffer's contents
+    hs = states.copy()
+    out = np.full_like(data, 0xA5)
+    brb.rc4_crypt_batch(hs, data, offs, lens, out=out)
+    mask = np.zeros(data.size, bool)
+    for o, n in zip(offs.tolist(), lens.tolist()):
+        mask[o:o + n] = True
+    assert np.array_equal(out[mask], want[mask]) and np.all(out[~mask] == 0xA5)
+    assert np.array_equal(hs, want_st)
+
+
+@pytest.mark.gpu
+def test_rc4_state_carries_across_calls(brb, orc, torch_dev):
+    n = 200
+    states = brb.rc4_states(_keys(n, 5))
+    ts = _to(torch_dev, states)
+    ost = states.copy()
+    for call in range(4):
+        lens = np.random.default_rng(call).integers(0, 300, n)
+        offs, lens, total = _layout(lens, 7 + call, call)
+        data = workload.gen_records(SEED + call, 0, 1, total + 4)
+        ost, want = _oracle_crypt(orc, ost, data, offs, lens)
+        t = _to(torch_dev, data)
+        brb.rc4_crypt_batch(ts, t, _to(torch_dev, offs), _to(torch_dev, lens))
+        assert np.array_equal(t.cpu().numpy(), want), call
+    assert np.array_equal(ts.cpu().numpy(), ost)
+
+
+@pytest.mark.gpu
+def test_rc4_golden_streams(brb, torch_dev, golden):
+    for v in golden["rc4"]["streams"]:
+        st = brb.rc4_states([bytes.fromhex(v["key"])])
+        data = np.frombuffer(bytes.fromhex(v["data"]), np.uint8).copy()
+        pos = 0
+        for n, want in zip(v["lens"], v["out"]):
+            seg = data[pos:pos + n].copy()
+            brb.rc4_crypt_batch(st, seg, np.array([0], np.uint64), np.array([n], np.uint32))
+            assert seg.tobytes().hex() == want
+            pos += n
+        assert st[0].tobytes().hex() == v["state_after"]
+
+
+def _oracle_frames(orc, states, payload, offs, lens, salts, frames, foffs):
+    st = states.copy()
+    fr = frames.copy()
+    for i in range(len(offs)):
+        o, n, fo = int(offs[i]), int(lens[i]), int(foffs[i])
+        s2, f = orc.rc4md5_frame(st[i].tobytes(), payload[o:o + n].tobytes(), int(salts[i]))
+        st[i] = np.frombuffer(s2, np.uint8)
+        fr[fo:fo + 30 + n] = np.frombuffer(f, np.uint8)
+    return st, fr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fbase", [0, 1, 2, 3])
+def test_rc4md5_frame_batch(brb, orc, torch_dev, fbase):
+    lens = (RAGGED * 4)[: 100]
+    offs, lens, total = _layout(lens, 3, 1)
+    payload = workload.gen_records(SEED, 7, 1, total + 4)
+    foffs, _, ftotal = _layout([30 + int(x) for x in lens], 9, fbase)
+    salts = np.array([(0x9E3779B9 * (i + 1)) & 0xFFFFFFFF for i in range(len(offs))], np.uint64)
+    states = brb.rc4_states(_keys(len(offs), 8))
+    frames0 = np.full(ftotal + 8, 0x5A, np.uint8)
+    want_st, want = _oracle_frames(orc, states, payload, offs, lens, salts, frames0, foffs)
+    # device mode
+    ts, tf = _to(torch_dev, states), _to(torch_dev, frames0)
+    brb.rc4md5_frame_batch(ts, _to(torch_dev, payload), _to(torch_dev, offs), _to(torch_dev, lens),
+                           _to(torch_dev, salts), tf, _to(torch_dev, foffs))
+    assert np.array_equal(tf.cpu().numpy(), want)
+    assert np.array_equal(ts.cpu().numpy(), want_st)
+    # host mode
+    hs, hf = states.copy(), frames0.copy()
+    brb.rc4md5_frame_batch(hs, payload, offs, lens, salts, hf, foffs)
+    assert np.array_equal(hf, want) and np.array_equal(hs, want_st)
+
+
+@pytest.mark.gpu
+def test_rc4md5_golden_frames(brb, golden):
+    for v in golden["rc4"]["frames"]:
+        payload = np.frombuffer(bytes.fromhex(v["payload"]) + b"\0", np.uint8).copy()
+        n = len(payload) - 1
+        st = brb.rc4_states([bytes.fromhex(v["key"])])
+        fr = np.zeros(30 + n, np.uint8)
+        brb.rc4md5_frame_batch(st, payload, np.array([0], np.uint64), np.array([n], np.uint32),
+                               np.array([v["salt"]], np.uint64), fr, np.array([0], np.uint64))
+        assert fr.tobytes().hex() == v["frame"] and st[0].tobytes().hex() == v["state_after"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("base", [0, 1, 2, 3])
+def test_rc4md5_open_batch(brb, orc, torch_dev, base):
+    """Frames written by the oracle are opened on the GPU; corrupted / short frames are rejected."""
+    lens = (RAGGED * 4)[: 108]
+    keys = _keys(len(lens), 12)
+    rng = np.random.default_rng(base)
+    frames, flens, expect_valid = [], [], []
+    for i, n in enumerate(lens):
+        payload = workload.gen_records(SEED, 100 + i, 1, n).tobytes() if n else b""
+        _, fr = orc.rc4md5_frame(orc.rc4_init(keys[i]), payload, i)
+        fr = bytearray(fr)
+        kind = i % 6
+        if kind == 3:                    # corrupt the tag, the digest or the payload
+            pos = int(rng.choice([8, 10, 12, 13, 20, 28] + ([30, len(fr) - 1] if n else [])))
+            fr[pos] ^= 0x40
+        elif kind == 5 and n < 40:       # truncated below the header
+            fr = fr[: int(rng.integers(0, 30))]
+        frames.append(bytes(fr))
+        flens.append(len(fr))
+    offs, flens, total = _layout(flens, 4, base)
+    buf = np.zeros(total + 8, np.uint8)
+    for o, f in zip(offs.tolist(), frames):
+        buf[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    states = brb.rc4_states(keys)
+    want_buf, want_st, want_ok = buf.copy(), states.copy(), []
+    for i, (o, f) in enumerate(zip(offs.tolist(), frames)):
+        s2, dec, ok = orc.rc4md5_open(states[i].tobytes(), f)
+        want_st[i] = np.frombuffer(s2, np.uint8)
+        want_buf[o:o + len(f)] = np.frombuffer(dec, np.uint8)
+        want_ok.append(ok)
+    want_ok = np.array(want_ok, np.uint8)
+    assert 0 < want_ok.sum() < len(want_ok)
+    # device mode, in place
+    ts, tb = _to(torch_dev, states), _to(torch_dev, buf)
+    _, valid = brb.rc4md5_open_batch(ts, tb, _to(torch_dev, offs), _to(torch_dev, flens))
+    assert np.array_equal(tb.cpu().numpy(), want_buf)
+    assert np.array_equal(ts.cpu().numpy(), want_st)
+    assert np.array_equal(valid.cpu().numpy(), want_ok)
+    # host mode, out of place
+    hs, out = states.copy(), np.zeros_like(buf)
+    _, hv = brb.rc4md5_open_batch(hs, buf, offs, flens, out=out)
+    assert np.array_equal(hv, want_ok) and np.array_equal(hs, want_st)
+    for o, n in zip(offs.tolist(), flens.tolist()):
+        assert np.array_equal(out[o:o + n], want_buf[o:o + n])
+
+
+@pytest.mark.gpu
+def test_rc4md5_round_trip_large(brb, torch_dev):
+    """Frame on the GPU, open on the GPU: 4096 connections x 1500 B plus a few 64 KiB payloads."""
+    torch = torch_dev
+    lens = [1500] * 4096 + [65536, 65535, 65537]
+    n = len(lens)
+    offs, lens, total = _layout(lens)
+    payload = workload.gen_records(SEED, 0, 1, total)
+    foffs, flens, ftotal = _layout([30 + int(x) for x in lens])
+    keys = _keys(n, 21)
+    wst, rst = _to(torch, brb.rc4_states(keys)), _to(torch, brb.rc4_states(keys))
+    frames = torch.zeros(ftotal, dtype=torch.uint8, device="cuda")
+    salts = _to(torch, np.arange(n, dtype=np.uint64))
+    brb.rc4md5_frame_batch(wst, _to(torch, payload), _to(torch, offs), _to(torch, lens), salts, frames,
+                           _to(torch, foffs))
+    _, valid = brb.rc4md5_open_batch(rst, frames, _to(torch, foffs), _to(torch, flens))
+    assert int(valid.sum()) == n
+    assert torch.equal(wst, rst)          # both ends consumed the same keystream
+    fr = frames.cpu().numpy()
+    for i in (0, 1, 4095, n - 1):
+        o, fo, m = int(offs[i]), int(foffs[i]), int(lens[i])
+        assert fr[fo + 30:fo + 30 + m].tobytes() == payload[o:o + m].tobytes()
+        assert fr[fo + 13:fo + 29].tobytes() == hashlib.md5(payload[o:o + m].tobytes()).digest()
