@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--op", default="md5", choices=["md5", "sha1"])
+    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5"],
+                    help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B)")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the timed steps alternate over")
     ap.add_argument("--two-stream", action="store_true", help="also time the steps over 2 streams")
@@ -119,7 +120,9 @@ def main():
     cfg = workload.CONFIGS[cfg_id]
     stream = torch.cuda.current_stream(dev)
 
-    if cfg["op"] == "blowfish":
+    if args.op in ("rc4", "rc4md5"):
+        result = bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
+    elif cfg["op"] == "blowfish":
         result = bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
     else:
         result = bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
@@ -375,6 +378,115 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
         result["cpu_baseline"] = {"value": round(sample.nbytes * reps / dt / 2**30, 3), "unit": "GiB/s",
                                   "cores": th, "kind": "port",
                                   "sample": f"oracle bf_ecb enc+dec over {sample.nbytes >> 20} MiB, {reps} passes"}
+    return result
+
+
+# ------------------------------------------------------------------------------------------------
+def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
+    """SURVEY §8 f1 on the cfg2 shape: 65 536 connections x 1500-byte payloads per GPU.
+    --op rc4:    one step = BRB_RC4_CryptBatch in place over every connection's buffer.
+    --op rc4md5: one step = BRB_RC4MD5_FrameBatch (write side) of every payload into a 1530-byte
+                 frame, then BRB_RC4MD5_OpenBatch (read side + validation) of those frames.
+    The RC4 states advance from step to step exactly as a connection's stream does."""
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+    import oracle
+
+    L = 1500
+    n = args.records_per_gpu or 65536
+    H = brb.RC4MD5_HEADER
+    host = workload.gen_records(workload.SEEDS[2], rank * n, n, L)
+    n_rot = max(2, math.ceil(640e6 / host.nbytes))
+    bufs = [torch.from_numpy(host).to(dev)]
+    for _ in range(n_rot - 1):
+        bufs.append(bufs[0].clone())
+    rng = np.random.default_rng(rank)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    st0 = brb.rc4_states(keys)
+    offs = torch.from_numpy(np.arange(n, dtype=np.uint64) * L).to(dev)
+    lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+    foffs = torch.from_numpy(np.arange(n, dtype=np.uint64) * (L + H)).to(dev)
+    flens = torch.full((n,), L + H, dtype=torch.int32, device=dev)
+    salts = torch.from_numpy(rng.integers(0, 2**32, n, dtype=np.uint64)).to(dev)
+    frames = torch.zeros(n * (L + H), dtype=torch.uint8, device=dev)
+    valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    wst, rst = torch.from_numpy(st0).to(dev), torch.from_numpy(st0).to(dev)
+    Lb = brb.lib()
+    flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
+    P = {k: v.data_ptr() for k, v in dict(offs=offs, lens=lens, foffs=foffs, flens=flens, salts=salts,
+                                           frames=frames, valid=valid, wst=wst, rst=rst).items()}
+    bptr = [b.data_ptr() for b in bufs]
+
+    def launch(k, s, j=0):
+        h = s.cuda_stream
+        if args.op == "rc4":
+            rc = Lb.BRB_RC4_CryptBatch(P["wst"], bptr[k % n_rot], bptr[k % n_rot], P["offs"], P["lens"], n, flags, h)
+        else:
+            rc = Lb.BRB_RC4MD5_FrameBatch(P["wst"], bptr[k % n_rot], P["offs"], P["lens"], P["salts"], P["frames"],
+                                          P["foffs"], n, flags, h)
+            if rc == 1:
+                rc = Lb.BRB_RC4MD5_OpenBatch(P["rst"], P["frames"], P["frames"], P["foffs"], P["flens"], n,
+                                             P["valid"], flags, h)
+        if rc != 1:
+            raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+
+    for k in range(args.warmup):
+        launch(k, stream)
+    torch.cuda.synchronize()
+    wall, ev_s = timed_steps(lambda k, s, j: launch(k + args.warmup, s, j), args.steps, [stream], barrier,
+                             max_over_ranks, torch)
+    if args.op == "rc4md5":
+        assert int(valid.sum()) == n, "a frame failed validation"
+        assert torch.equal(wst, rst), "write and read states diverged"
+        fr = frames[: 2 * (L + H)].cpu().numpy()
+        assert fr[H:H + L].tobytes() == host[:L].tobytes()      # decrypted in place by the open step
+    step_s = ev_s / args.steps
+    payload = n * L
+    moved = 2 * payload if args.op == "rc4" else payload + 3 * n * (L + H)
+    name = "BRB_RC4_CryptBatch" if args.op == "rc4" else "BRB_RC4MD5_FrameBatch + BRB_RC4MD5_OpenBatch"
+    result = {
+        "metric": f"GiB/s of payload per {'RC4 pass' if args.op == 'rc4' else 'RC4+MD5 frame + open round trip'} "
+                  "(SURVEY §8 f1)",
+        "value": round(payload * world * args.steps / wall / 2**30, 2),
+        "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic (splitmix64 payloads, HBM-resident, {n_rot} rotating copies; random 16-byte keys)",
+        "config": {"workload": f"f1: {n} connections x {L} B, 1 GPU" if world == 1 else f"f1: {n} connections/GPU",
+                   "op": name + " (device mode)", "records_per_gpu": n, "record_bytes": L,
+                   "parallelism": f"connection-shard x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(moved / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
+                     "note": "algorithmic bytes read+written per step; the bound in practice is the per-byte "
+                             "RC4 dependency chain through LDS (DESIGN.md)"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op == "rc4md5":
+        th = cpu_threads()
+        m = min(n, 16384)
+        hst = st0[:m].copy()
+        ho = np.arange(m, dtype=np.uint64) * L
+        hl = np.full(m, L, np.uint32)
+        hfo = np.arange(m, dtype=np.uint64) * (L + H)
+        hfl = np.full(m, L + H, np.uint32)
+        hs = np.arange(m, dtype=np.uint64)
+        hf = np.zeros(m * (L + H), np.uint8)
+        hv = np.zeros(m, np.uint8)
+        rs = st0[:m].copy()
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            oracle.rc4md5_frame_batch(hst, host, ho, hl, hs, hf, hfo, threads=th)
+            oracle.rc4md5_open_batch(rs, hf, hfo, hfl, hv, threads=th)
+            reps += 1
+        dt = time.perf_counter() - t0
+        assert hv.all()
+        result["cpu_baseline"] = {"value": round(m * L * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": th,
+                                  "kind": "port",
+                                  "sample": f"oracle frame+open of {m} connections x {L} B, {reps} passes, {th} pthreads"}
+    log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")
     return result
 
 

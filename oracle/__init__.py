@@ -49,6 +49,8 @@ def lib() -> ctypes.CDLL:
             "orc_rc4_crypt": (None, [vp, vp, vp, ctypes.c_int]),
             "orc_rc4md5_frame": (None, [vp, vp, u64, u64, vp]),
             "orc_rc4md5_open": (ctypes.c_int, [vp, vp, u64]),
+            "orc_rc4md5_frame_batch": (None, [vp, vp, vp, vp, vp, vp, vp, u64, ctypes.c_int]),
+            "orc_rc4md5_open_batch": (None, [vp, vp, vp, vp, u64, vp, ctypes.c_int]),
             "orc_splitmix64": (u64, [u64]),
             "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
         }
@@ -201,6 +203,16 @@ def rc4md5_open(state: bytes, frame: bytes) -> tuple[bytes, bytes, int]:
     fr = ctypes.create_string_buffer(bytes(frame), max(len(frame), 1))
     ok = lib().orc_rc4md5_open(st, fr, len(frame))
     return st.raw, fr.raw[: len(frame)], ok
+
+
+def rc4md5_frame_batch(states, payload, offs, lens, salts, frames, foffs, threads=1):
+    """n connections at once (numpy arrays; states (n, 264) uint8 updated in place)."""
+    lib().orc_rc4md5_frame_batch(_p(states), _p(payload), _p(offs), _p(lens), _p(salts), _p(frames), _p(foffs),
+                                 len(offs), threads)
+
+
+def rc4md5_open_batch(states, frames, offs, lens, valid, threads=1):
+    lib().orc_rc4md5_open_batch(_p(states), _p(frames), _p(offs), _p(lens), len(offs), _p(valid), threads)
 
 
 # ---- generator (SURVEY.md §8(d)) ---------------------------------------------------------------

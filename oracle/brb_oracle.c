@@ -566,6 +566,63 @@ int orc_rc4md5_open(orc_rc4_state *s, uint8_t *frame, uint64_t frame_len)
     return memcmp(dig, frame + 13, 16) == 0;
 }
 
+typedef struct {
+    orc_rc4_state *s;
+    const uint8_t *payload;
+    uint8_t *frames;
+    const uint64_t *off, *foff, *salts;
+    const uint32_t *len;
+    uint8_t *valid;
+    uint64_t r0, r1;
+} rc4_job;
+
+static void *rc4_frame_worker(void *arg)
+{
+    rc4_job *j = (rc4_job *)arg;
+    for (uint64_t r = j->r0; r < j->r1; r++)
+        orc_rc4md5_frame(&j->s[r], j->payload + j->off[r], j->len[r], j->salts[r], j->frames + j->foff[r]);
+    return NULL;
+}
+
+static void *rc4_open_worker(void *arg)
+{
+    rc4_job *j = (rc4_job *)arg;
+    for (uint64_t r = j->r0; r < j->r1; r++)
+        j->valid[r] = (uint8_t)orc_rc4md5_open(&j->s[r], j->frames + j->off[r], j->len[r]);
+    return NULL;
+}
+
+static void rc4_run(rc4_job proto, uint64_t n, int n_threads, void *(*fn)(void *))
+{
+    pthread_once(&md5_once, md5_tables);
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    rc4_job jobs[256];
+    for (int t = 0; t < n_threads; t++) {
+        jobs[t] = proto;
+        jobs[t].r0 = n * (uint64_t)t / (uint64_t)n_threads;
+        jobs[t].r1 = n * (uint64_t)(t + 1) / (uint64_t)n_threads;
+    }
+    if (n_threads == 1) { fn(&jobs[0]); return; }
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, fn, &jobs[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_rc4md5_frame_batch(orc_rc4_state *s, const uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                            const uint64_t *salts, uint8_t *frames, const uint64_t *foff, uint64_t n, int n_threads)
+{
+    rc4_job p = {s, payload, frames, off, foff, salts, len, NULL, 0, 0};
+    rc4_run(p, n, n_threads, rc4_frame_worker);
+}
+
+void orc_rc4md5_open_batch(orc_rc4_state *s, uint8_t *frames, const uint64_t *off, const uint32_t *len, uint64_t n,
+                           uint8_t *valid, int n_threads)
+{
+    rc4_job p = {s, NULL, frames, off, NULL, NULL, len, valid, 0, 0};
+    rc4_run(p, n, n_threads, rc4_open_worker);
+}
+
 /* =========================================================================================== */
 /* Generator                                                                                     */
 /* =========================================================================================== */

@@ -103,6 +103,11 @@ void orc_rc4_crypt(orc_rc4_state *s, const unsigned char *in, unsigned char *out
 #define ORC_RC4MD5_HDR 30
 void orc_rc4md5_frame(orc_rc4_state *s, const uint8_t *payload, uint64_t len, uint64_t salt, uint8_t *frame);
 int orc_rc4md5_open(orc_rc4_state *s, uint8_t *frame, uint64_t frame_len);
+/* n connections (pthreads over contiguous connection ranges; bench.py's cpu_baseline) */
+void orc_rc4md5_frame_batch(orc_rc4_state *s, const uint8_t *payload, const uint64_t *off, const uint32_t *len,
+                            const uint64_t *salts, uint8_t *frames, const uint64_t *foff, uint64_t n, int n_threads);
+void orc_rc4md5_open_batch(orc_rc4_state *s, uint8_t *frames, const uint64_t *off, const uint32_t *len, uint64_t n,
+                           uint8_t *valid, int n_threads);
 
 /* ---- Batches (used by tests and by bench.py's cpu_baseline) ------------------------------- */
 void orc_md5_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out16, int n_threads);

@@ -7,6 +7,7 @@
  *   - RC4+MD5 frame validation digest + memcmp of 16 bytes       (event/aio/ev_kq_aio_transform.c:175-180)
  *   - RSA-SHA1 signing pre-digest: BrbSha1_Do                    (comm/utils/comm_ssl_pkey.c:465)
  *   - MemBuffer Blowfish ECB over word pairs                     (data/core/mem_buf.c:1528-1539)
+ *   - RC4 connection streams: Init per direction, Crypt per buffer (ev_kq_aio_transform.c:89-90,273,282)
  *   - then the batch surface on the same records, which must agree with the compat results
  *     (returns 0 with a reason when no GPU is present; it never computes on the CPU).
  *
@@ -81,6 +82,22 @@ int main(void)
     printf("bf_roundtrip %d\n", memcmp(w, w0, sizeof(w)) == 0);
     printf("bf_enc0 %016lx%016lx\n", enc[0], enc[1]);
 
+    /* RC4: write and read states from one key; two buffers on the write stream, decrypted in one
+     * read call; the "Key"/"Plaintext" vector on a fresh state */
+    BRB_RC4_State wst, rst, kst;
+    BRB_RC4_Init(&wst, (const unsigned char *)"cryptokey", 9);
+    BRB_RC4_Init(&rst, (const unsigned char *)"cryptokey", 9);
+    static unsigned char c1[RLEN], p1[RLEN];
+    BRB_RC4_Crypt(&wst, recs, c1, 700);
+    BRB_RC4_Crypt(&wst, recs + 700, c1 + 700, RLEN - 700);
+    BRB_RC4_Crypt(&rst, c1, p1, RLEN);
+    printf("rc4_roundtrip %d\n", memcmp(p1, recs, RLEN) == 0 && memcmp(&wst, &rst, sizeof(wst)) == 0);
+    unsigned char kc[9];
+    BRB_RC4_Init(&kst, (const unsigned char *)"Key", 3);
+    BRB_RC4_Crypt(&kst, (const unsigned char *)"Plaintext", kc, 9);
+    hex(kc, 9, h);
+    printf("rc4_kat %s\n", h);
+
     /* batch surface on the same data (host mode) */
     static unsigned char dig16[NREC][16], dig20[NREC][20];
     int rc = BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_HOST, NULL);
@@ -95,5 +112,13 @@ int main(void)
     memcpy(w, w0, sizeof(w));
     rc = BRB_Blowfish_EncryptBatch(&bf, w, 32, BRB_BATCH_HOST, NULL);
     printf("batch_bf_eq %d\n", rc == 1 && memcmp(w, enc, sizeof(enc)) == 0);
+    /* RC4 batch: one stream of 1500 B on a fresh write state must equal c1 (the two compat calls) */
+    BRB_RC4_State bst;
+    BRB_RC4_Init(&bst, (const unsigned char *)"cryptokey", 9);
+    static unsigned char bc[RLEN];
+    uint64_t off0 = 0;
+    uint32_t len0 = RLEN;
+    rc = BRB_RC4_CryptBatch(&bst, recs, bc, &off0, &len0, 1, BRB_BATCH_HOST, NULL);
+    printf("batch_rc4_eq %d\n", rc == 1 && memcmp(bc, c1, RLEN) == 0 && memcmp(&bst, &wst, sizeof(bst)) == 0);
     return 0;
 }

@@ -81,9 +81,11 @@ def test_unchanged_c_caller_links_and_agrees(brb, tmp_path):
     assert res["meta_md5"] == hashlib.md5(recs[:4500]).hexdigest()
     assert res["rec_last_md5"] == hashlib.md5(recs[-1500:]).hexdigest()
     assert res["rec_last_sha1"] == hashlib.sha1(recs[-1500:]).hexdigest()
-    assert res["validate"] == "1" and res["bf_roundtrip"] == "1"
+    assert res["validate"] == "1" and res["bf_roundtrip"] == "1" and res["rc4_roundtrip"] == "1"
+    assert res["rc4_kat"] == "bbf316e8d940af0ad3"
     if res["batch_md5_rc"] == "1":          # GPU present: batch == compat
         assert res["batch_md5_eq"] == "1" and res["batch_sha1_eq"] == "1" and res["batch_bf_eq"] == "1"
+        assert res["batch_rc4_eq"] == "1"
     else:                                   # no GPU: refused with a reason, no CPU fallback
         assert res["batch_md5_rc"] == "0" and res["batch_reason"].strip()
 

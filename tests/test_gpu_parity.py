@@ -209,3 +209,4 @@ def test_c_caller_batch_on_gpu(brb, tmp_path):
     res = run_caller(build_caller(tmp_path))
     assert res["batch_md5_rc"] == "1"
     assert res["batch_md5_eq"] == "1" and res["batch_sha1_eq"] == "1" and res["batch_bf_eq"] == "1"
+    assert res["batch_rc4_eq"] == "1"
