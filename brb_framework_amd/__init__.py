@@ -31,6 +31,10 @@ from .crypto import (  # noqa: F401
     lib,
     md5_batch,
     md5_batch_fixed,
+    membuf_decrypt,
+    membuf_encrypt,
+    membuf_key,
+    membuf_span,
     rc4_crypt_batch,
     rc4_init,
     rc4_state_bytes,
@@ -46,5 +50,6 @@ __all__ = [
     "LIB_PATH", "blowfish_ctx_bytes", "blowfish_decrypt_batch", "blowfish_encrypt_batch",
     "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
     "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
-    "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch",
+    "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
+    "membuf_encrypt", "membuf_key", "membuf_span",
 ]

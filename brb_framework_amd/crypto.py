@@ -95,6 +95,13 @@ _SIGNATURES = [
     ("BRB_RC4MD5_OpenBatch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
       ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_MemBufferKey", None, [ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_MemBufferEncrypt", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_ulong, ctypes.POINTER(ctypes.c_ulong), ctypes.c_uint,
+      ctypes.c_void_p]),
+    ("BRB_MemBufferDecrypt", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_ulong, ctypes.POINTER(ctypes.c_ulong), ctypes.c_uint,
+      ctypes.c_void_p]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
@@ -320,3 +327,35 @@ def rc4md5_open_batch(states, frames, offsets, lengths, out=None, valid=None, st
     _check(lib().BRB_RC4MD5_OpenBatch(_ptr(states), _ptr(frames), _ptr(out), _ptr(offsets), _ptr(lengths), n,
                                       _ptr(valid), flags, h), "BRB_RC4MD5_OpenBatch")
     return out, valid
+
+
+# ---- MemBuffer Blowfish ------------------------------------------------------------
+def membuf_span(size: int, offset: int) -> int:
+    """BRB_MEMBUF_SPAN: bytes the call touches after buf + offset."""
+    return (((size + offset) // 8 + 3) // 2) * 16
+
+
+def membuf_key(seed: int) -> bytes:
+    k = (ctypes.c_uint * 16)()
+    lib().BRB_MemBufferKey(seed, k)
+    return bytes(k)
+
+
+def _membuf(fn, buf, size, seed, offset, stream):
+    need = offset + membuf_span(size, offset)
+    if _nbytes(buf) < need:
+        raise ValueError(f"buffer holds {_nbytes(buf)} bytes, the call needs {need}")
+    flags, h = _mode(buf, stream, False)
+    ns = ctypes.c_ulong(0)
+    _check(fn(_ptr(buf), size, seed, offset, ctypes.byref(ns), flags, h), fn.__name__)
+    return ns.value
+
+
+def membuf_encrypt(buf, size, seed, offset=0, stream=None):
+    """BRB_MemBufferEncrypt in place; returns the new MemBuffer size."""
+    return _membuf(lib().BRB_MemBufferEncrypt, buf, size, seed, offset, stream)
+
+
+def membuf_decrypt(buf, size, seed, offset=0, stream=None):
+    """BRB_MemBufferDecrypt in place; returns the new MemBuffer size."""
+    return _membuf(lib().BRB_MemBufferDecrypt, buf, size, seed, offset, stream)

@@ -443,9 +443,93 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
     return rc;
 }
 
+// ---- MemBuffer Blowfish -------------------------------------------------------
+int membuf_crypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset, unsigned long *new_size,
+                 unsigned flags, void *stream, bool decrypt)
+{
+    t_err.clear();
+    if (!buf || !new_size) {
+        set_err("NULL buf or new_size");
+        return BRB_BATCH_BADARG;
+    }
+    if (decrypt && size < offset) {
+        set_err("size %lu < offset %lu (the reference would walk ~2^61 words)", size, offset);
+        return BRB_BATCH_BADARG;
+    }
+    uint8_t *raw = static_cast<uint8_t *>(buf) + offset;
+    if ((flags & BRB_BATCH_DEVICE) && (reinterpret_cast<uintptr_t>(raw) & 7)) {
+        set_err("device mode needs buf + offset 8-byte aligned");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    // host side: key (mem_buf.c:1511-1515) and the reference's keyLen quirk (:1528 vs :1582)
+    unsigned int key[16];
+    BRB_MemBufferKey(seed, key);
+    BRB_BLOWFISH_CTX *ctx = static_cast<BRB_BLOWFISH_CTX *>(malloc(sizeof(BRB_BLOWFISH_CTX)));
+    if (!ctx) {
+        set_err("out of host memory");
+        return BRB_BATCH_NOT_DONE;
+    }
+    BRB_Blowfish_Init(ctx, reinterpret_cast<unsigned char *>(key), decrypt ? int(sizeof(key)) : int(sizeof(key[0])));
+    const uint64_t words = (decrypt ? (size - offset) : (size + offset)) / 8 + 2;
+    const uint64_t pairs = (words + 1) / 2;
+    const size_t span = size_t(16) * pairs;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    Staging st;
+    const size_t i_ctx = st.add(ctx, nullptr, sizeof(BRB_BLOWFISH_CTX));
+    const size_t i_first = st.add(nullptr, nullptr, 8);
+    const size_t i_w = (flags & BRB_BATCH_DEVICE) ? 0 : st.add(raw, raw, span);
+    int rc = st.upload(s);
+    uint64_t *w = (flags & BRB_BATCH_DEVICE) ? reinterpret_cast<uint64_t *>(raw) : reinterpret_cast<uint64_t *>(st.dev(i_w));
+    unsigned long long done = pairs;
+    if (rc == BRB_BATCH_OK && decrypt) {
+        unsigned long long *first = reinterpret_cast<unsigned long long *>(st.dev(i_first));
+        if ((e = hipMemcpyAsync(first, &done, 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+            rc = fail_hip("hipMemcpyAsync H2D", e);
+        else if ((e = brb::launch_first_zero_pair(w, pairs, first, s)) != hipSuccess)
+            rc = fail_hip("kernel launch", e);
+        else if ((e = hipMemcpyAsync(&done, first, 8, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                 (e = hipStreamSynchronize(s)) != hipSuccess)
+            rc = fail_hip("zero-pair scan", e);
+    }
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_blowfish(reinterpret_cast<const uint64_t *>(st.dev(i_ctx)), w, done, decrypt, s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        rc = st.download(s);        // host mode: the staged words back; always: synchronise
+    else
+        (void)hipStreamSynchronize(s);
+    free(ctx);
+    if (rc == BRB_BATCH_OK)
+        *new_size = static_cast<unsigned long>(16 * done + offset);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
+
+void BRB_MemBufferKey(unsigned int seed, unsigned int key[16])
+{
+    for (unsigned long i = 0; i < 16; i++) {          // mem_buf.c:1511-1515 (unsigned long i)
+        key[i] = static_cast<unsigned int>(((i + seed) * seed) + (13 * i));
+        seed = key[i] * seed;
+    }
+}
+
+int BRB_MemBufferEncrypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset, unsigned long *new_size,
+                         unsigned flags, void *hip_stream)
+{
+    return membuf_crypt(buf, size, seed, offset, new_size, flags, hip_stream, false);
+}
+
+int BRB_MemBufferDecrypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset, unsigned long *new_size,
+                         unsigned flags, void *hip_stream)
+{
+    return membuf_crypt(buf, size, seed, offset, new_size, flags, hip_stream, true);
+}
 
 int BRB_MD5BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec, unsigned char (*digests)[16], unsigned flags,
                       void *hip_stream)

@@ -24,9 +24,33 @@ int cu_count()
     return n;
 }
 
+// MemBufferDecryptData's "padding gremlin" stop (mem_buf.c:1595-1596): first pair with a zero word
+__global__ __launch_bounds__(256) void first_zero_pair_kernel(const uint64_t *__restrict__ w, uint64_t n,
+                                                              unsigned long long *first)
+{
+    unsigned long long best = ~0ull;
+    for (uint64_t b = uint64_t(blockIdx.x) * 256 + threadIdx.x; b < n; b += uint64_t(gridDim.x) * 256)
+        if (w[2 * b] == 0 || w[2 * b + 1] == 0) {
+            best = b;
+            break;        // later b of this lane are larger
+        }
+    if (best != ~0ull)
+        atomicMin(first, best);
+}
+
 }  // namespace
 
 namespace brb {
+
+hipError_t launch_first_zero_pair(const uint64_t *words, uint64_t n_blocks, unsigned long long *first, hipStream_t s)
+{
+    if (n_blocks == 0)
+        return hipSuccess;
+    const uint64_t want = (n_blocks + 255) / 256;
+    const unsigned g = unsigned(want < 2048 ? want : 2048);
+    first_zero_pair_kernel<<<g, 256, 0, s>>>(words, n_blocks, first);
+    return hipGetLastError();
+}
 
 hipError_t launch_blowfish(const uint64_t *ctx_dev, uint64_t *words, uint64_t n_blocks, bool decrypt, hipStream_t s)
 {

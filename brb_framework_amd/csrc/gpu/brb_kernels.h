@@ -17,6 +17,8 @@ hipError_t launch_sha1_var(const uint8_t *data, const uint64_t *offs, const uint
                            uint8_t *out, hipStream_t s);
 // ctx_dev: device copy of BRB_BLOWFISH_CTX (P[18] then S[4][256], 64-bit words)
 hipError_t launch_blowfish(const uint64_t *ctx_dev, uint64_t *words, uint64_t n_blocks, bool decrypt, hipStream_t s);
+// *first = min(*first, index of the first block (xl, xr) with a zero word); *first preset by the caller
+hipError_t launch_first_zero_pair(const uint64_t *words, uint64_t n_blocks, unsigned long long *first, hipStream_t s);
 
 // RC4 (rc4_kernels.hip): states = n contiguous 264-byte BRB_RC4_State, updated in place
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,

@@ -179,6 +179,26 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
                          const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags,
                          void *hip_stream);
 
+/* ---- MemBuffer Blowfish -------------------------------------------------------
+ * MemBufferEncryptData / MemBufferDecryptData (mem_buf.c:1499-1617) on the bytes of a MemBuffer:
+ * buf = MemBufferDeref(mb) with mb->offset == 0, size = MemBufferGetSize(mb).  Reproduced exactly:
+ *   key[i] = (i + seed) * seed + 13 i, seed = key[i] * seed            (mem_buf.c:1511-1515)
+ *   encrypt: Blowfish keyLen 4 (sizeof(enc_key[16])), pairs of 64-bit words from buf + offset,
+ *            (size + offset) / 8 + 2 words rounded up to pairs; new size = 8 * words + offset
+ *   decrypt: keyLen 64 (sizeof(enc_key)), (size - offset) / 8 + 2 words, stops at the first pair
+ *            holding a zero word; new size = 8 * words decrypted + offset
+ * (so decrypt(encrypt(x)) does not restore x, as in the reference).  The caller grows the buffer
+ * first, as MemBufferCheckForGrow does (mem_buf.c:1525, 1585): buf must hold
+ * offset + BRB_MEMBUF_SPAN(size, offset) bytes.  The Blowfish context is built on the host; the
+ * ECB pass (and the zero-pair scan) run on the GPU.  Device mode needs buf + offset 8-byte
+ * aligned.  Both calls return when *new_size is known (ASYNC is ignored). */
+#define BRB_MEMBUF_SPAN(size, offset) (((((size) + (offset)) / 8 + 3) / 2) * 16)
+void BRB_MemBufferKey(unsigned int seed, unsigned int key[16]);
+int BRB_MemBufferEncrypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset,
+                         unsigned long *new_size, unsigned flags, void *hip_stream);
+int BRB_MemBufferDecrypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset,
+                         unsigned long *new_size, unsigned flags, void *hip_stream);
+
 /* ---- runtime ---------------------------------------------------------------------------- */
 /* 1 if a HIP device is usable from this process, else 0 (reason in LastError). */
 int BRB_CryptoGPU_Available(void);
