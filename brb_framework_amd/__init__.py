@@ -31,6 +31,7 @@ from .crypto import (  # noqa: F401
     lib,
     md5_batch,
     md5_batch_fixed,
+    md5_batch_segments,
     membuf_decrypt,
     membuf_encrypt,
     membuf_key,
@@ -51,5 +52,5 @@ __all__ = [
     "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
     "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
-    "membuf_encrypt", "membuf_key", "membuf_span",
+    "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments",
 ]

@@ -77,6 +77,9 @@ _SIGNATURES = [
     ("BRB_MD5Batch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint,
       ctypes.c_void_p]),
+    ("BRB_MD5BatchSegments", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+      ctypes.c_uint, ctypes.c_void_p]),
     ("BrbSha1_BatchFixed", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
     ("BrbSha1_Batch", ctypes.c_int,
@@ -222,6 +225,18 @@ def sha1_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False)
 def md5_batch(data, offsets, lengths, out=None, stream=None, async_=False):
     """BRB_MD5Batch: offsets uint64[n], lengths uint32[n] (same memory kind as data)."""
     return _digest_var(lib().BRB_MD5Batch, 16, data, offsets, lengths, out, stream, async_)
+
+
+def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, stream=None, async_=False):
+    """BRB_MD5BatchSegments: record i = concatenation of segments rec_first_seg[i] .. rec_first_seg[i+1]-1
+    (the MetaData pack digest).  rec_first_seg has n + 1 entries."""
+    n = len(rec_first_seg) - 1
+    if out is None:
+        out = _out_like(data, n, 16)
+    flags, h = _mode(data, stream, async_)
+    _check(lib().BRB_MD5BatchSegments(_ptr(data), _ptr(seg_offsets), _ptr(seg_lengths), _ptr(rec_first_seg), n,
+                                      _ptr(out), flags, h), "BRB_MD5BatchSegments")
+    return out
 
 
 def sha1_batch(data, offsets, lengths, out=None, stream=None, async_=False):

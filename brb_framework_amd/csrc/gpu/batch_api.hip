@@ -443,6 +443,58 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
     return rc;
 }
 
+int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, const uint64_t *first, uint64_t n_rec,
+                 void *digests, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n_rec == 0)
+        return BRB_BATCH_OK;
+    if (!digests || !first || (!data || !soff || !slen)) {
+        set_err("NULL data, seg_offsets, seg_lengths, rec_first_seg or digests");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        e = brb::launch_md5_segments(static_cast<const uint8_t *>(data), soff, slen, first, n_rec,
+                                     static_cast<uint8_t *>(digests), s);
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    // host mode: rebase the segment lists to start at 0 and copy the byte span they cover
+    const uint64_t k0 = first[0], nseg = first[n_rec] - k0;
+    for (uint64_t i = 0; i < n_rec; i++)
+        if (first[i + 1] < first[i]) {
+            set_err("rec_first_seg is not non-decreasing at %llu", (unsigned long long)i);
+            return BRB_BATCH_BADARG;
+        }
+    uint64_t lo, hi;
+    span_of(soff + k0, slen + k0, nseg, 0, lo, hi);
+    const std::vector<uint64_t> roff = rebase(soff + k0, nseg, lo);
+    std::vector<uint64_t> rfirst(first, first + n_rec + 1);
+    for (uint64_t &f : rfirst)
+        f -= k0;
+    Staging st;
+    const size_t i_d = st.add(static_cast<const uint8_t *>(data) + lo, nullptr, size_t(hi - lo));
+    const size_t i_o = st.add(roff.data(), nullptr, 8 * nseg);
+    const size_t i_l = st.add(slen + k0, nullptr, 4 * nseg);
+    const size_t i_f = st.add(rfirst.data(), nullptr, 8 * (n_rec + 1));
+    const size_t i_out = st.add(nullptr, digests, 16 * n_rec);
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_md5_segments(st.dev(i_d), reinterpret_cast<const uint64_t *>(st.dev(i_o)),
+                                      reinterpret_cast<const uint32_t *>(st.dev(i_l)),
+                                      reinterpret_cast<const uint64_t *>(st.dev(i_f)), n_rec, st.dev(i_out), s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
 // ---- MemBuffer Blowfish -------------------------------------------------------
 int membuf_crypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset, unsigned long *new_size,
                  unsigned flags, void *stream, bool decrypt)
@@ -541,6 +593,13 @@ int BRB_MD5Batch(const void *data, const uint64_t *offsets, const uint32_t *leng
                  unsigned char (*digests)[16], unsigned flags, void *hip_stream)
 {
     return digest_var(brb::launch_md5_var, 16, data, offsets, lengths, n_rec, digests, flags, hip_stream);
+}
+
+int BRB_MD5BatchSegments(const void *data, const uint64_t *seg_offsets, const uint32_t *seg_lengths,
+                         const uint64_t *rec_first_seg, uint64_t n_rec, unsigned char (*digests)[16], unsigned flags,
+                         void *hip_stream)
+{
+    return md5_segments(data, seg_offsets, seg_lengths, rec_first_seg, n_rec, digests, flags, hip_stream);
 }
 
 int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec, uint8_t (*digests)[20], unsigned flags,

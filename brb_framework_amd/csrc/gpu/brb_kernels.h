@@ -20,6 +20,10 @@ hipError_t launch_blowfish(const uint64_t *ctx_dev, uint64_t *words, uint64_t n_
 // *first = min(*first, index of the first block (xl, xr) with a zero word); *first preset by the caller
 hipError_t launch_first_zero_pair(const uint64_t *words, uint64_t n_blocks, unsigned long long *first, hipStream_t s);
 
+// MD5 of segment lists (md5_seg_kernels.hip): record r = segments first[r] .. first[r + 1] - 1
+hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const uint32_t *slen, const uint64_t *first,
+                               uint64_t n_rec, uint8_t *out, hipStream_t s);
+
 // RC4 (rc4_kernels.hip): states = n contiguous 264-byte BRB_RC4_State, updated in place
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n, hipStream_t s);

@@ -130,6 +130,14 @@ int BRB_MD5BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec,
 int BRB_MD5Batch(const void *data, const uint64_t *offsets, const uint32_t *lengths,
                  uint64_t n_rec, unsigned char (*digests)[16], unsigned flags, void *hip_stream);
 
+/* MD5 of segment lists: record i is the concatenation of segments
+ * rec_first_seg[i] .. rec_first_seg[i + 1] - 1 (rec_first_seg has n_rec + 1 entries), segment k =
+ * data[seg_offsets[k] .. + seg_lengths[k]).  digests[i] = BRB_MD5Init, BRB_MD5UpdateBig per segment,
+ * BRB_MD5Final -- the MetaData pack digest of meta_data.c:397-433 with one record per MetaData. */
+int BRB_MD5BatchSegments(const void *data, const uint64_t *seg_offsets, const uint32_t *seg_lengths,
+                         const uint64_t *rec_first_seg, uint64_t n_rec, unsigned char (*digests)[16],
+                         unsigned flags, void *hip_stream);
+
 /* SHA-1 batches: digests[i] = BrbSha1_Do(record i) (20 raw big-endian bytes).  Unlike
  * BrbSha1_Update the batch surface never writes into the input records. */
 int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec,

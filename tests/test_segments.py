@@ -1,0 +1,81 @@
+"""MD5 of segment lists: the MetaData pack digest (meta_data.c:397-433: Init,
+UpdateBig per item, Final) batched as BRB_MD5BatchSegments, against the oracle's streaming MD5 (and
+hashlib) on the concatenation of each record's segments."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev(brb):
+    import torch
+    assert torch.cuda.is_available(), "no HIP device visible to torch"
+    assert brb.gpu_available(), brb.lib().BRB_CryptoGPU_LastError()
+    return torch
+
+
+def _case(seed, n_rec, max_segs, max_len):
+    rng = np.random.default_rng(seed)
+    seg_counts = rng.integers(0, max_segs + 1, n_rec)
+    first = np.zeros(n_rec + 1, np.uint64)
+    first[1:] = np.cumsum(seg_counts)
+    nseg = int(first[-1])
+    lens = rng.integers(0, max_len + 1, nseg).astype(np.uint32)
+    lens[rng.random(nseg) < 0.2] = rng.integers(0, 4, int((rng.random(nseg) < 0.2).sum()) or 1)[0]
+    pool = workload.gen_records(0x5EED00F4 + seed, 0, 1, int(lens.sum()) + 4096)
+    offs = rng.integers(0, pool.size - max_len - 1, nseg).astype(np.uint64)   # scattered, overlapping
+    return pool, offs, lens, first
+
+
+def _want(orc, pool, offs, lens, first):
+    out = []
+    for i in range(len(first) - 1):
+        msg = b"".join(pool[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+                       for k in range(int(first[i]), int(first[i + 1])))
+        out.append(hashlib.md5(msg).digest())
+    return np.frombuffer(b"".join(out), np.uint8).reshape(-1, 16)
+
+
+@pytest.mark.parametrize("seed,n_rec,max_segs,max_len", [(1, 300, 5, 40), (2, 200, 20, 7), (3, 64, 3, 3000),
+                                                        (4, 1000, 1, 200), (5, 5, 200, 100)])
+def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len):
+    pool, offs, lens, first = _case(seed, n_rec, max_segs, max_len)
+    want = _want(orc, pool, offs, lens, first)
+    got = brb.md5_batch_segments(pool, offs, lens, first)
+    assert np.array_equal(got, want)
+    t = torch_dev
+    dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
+                                 t.from_numpy(first).cuda())
+    assert np.array_equal(dev.cpu().numpy(), want)
+
+
+def test_segments_equal_streaming_oracle(brb, orc):
+    """The oracle's BRB_MD5Init/UpdateBig/Final restatement over the items = the batch digest."""
+    import ctypes
+    pool, offs, lens, first = _case(9, 50, 6, 100)
+    got = brb.md5_batch_segments(pool, offs, lens, first)
+    for i in range(50):
+        c = orc.Md5Ctx()
+        orc.lib().orc_md5_init(ctypes.byref(c))
+        for k in range(int(first[i]), int(first[i + 1])):
+            seg = pool[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+            orc.lib().orc_md5_update_big(ctypes.byref(c), seg, len(seg))
+        orc.lib().orc_md5_final(ctypes.byref(c))
+        assert bytes(c.digest) == got[i].tobytes()
+
+
+def test_segments_empty_and_sub_ranges(brb):
+    pool = np.arange(100, dtype=np.uint8)
+    # records: no segments, one empty segment, one segment; first[] not starting at 0
+    first = np.array([3, 3, 4, 5], np.uint64)
+    offs = np.array([0, 0, 0, 50, 10], np.uint64)
+    lens = np.array([9, 9, 9, 0, 33], np.uint32)
+    got = brb.md5_batch_segments(pool, offs, lens, first)
+    assert got[0].tobytes() == hashlib.md5(b"").digest()
+    assert got[1].tobytes() == hashlib.md5(b"").digest()
+    assert got[2].tobytes() == hashlib.md5(pool[10:43].tobytes()).digest()
