@@ -1,5 +1,5 @@
 """brb_framework_amd -- MI355X-native libbrb_core/crypto (MD5, SHA-1, 64-bit-word Blowfish, RC4 and
-the RC4+MD5 frame of the comm transform).
+the RC4+MD5 frame of the comm transform, MemBuffer Blowfish, MetaData digests, base64).
 
 The product is the C-ABI shared library ``libbrb_crypto_gpu.so`` built in this directory
 (``make -C brb_framework_amd``); its interface is ``include/brb_crypto.h``.  This Python package is
@@ -22,6 +22,8 @@ from .crypto import (  # noqa: F401
     RC4MD5_HEADER,
     BrbSha1Ctx,
     LIB_PATH,
+    base64_decode_batch,
+    base64_encode_batch,
     blowfish_ctx_bytes,
     blowfish_decrypt_batch,
     blowfish_encrypt_batch,
@@ -52,5 +54,6 @@ __all__ = [
     "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
     "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
-    "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments",
+    "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "base64_decode_batch",
+    "base64_encode_batch",
 ]

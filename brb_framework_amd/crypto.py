@@ -98,6 +98,12 @@ _SIGNATURES = [
     ("BRB_RC4MD5_OpenBatch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
       ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_Base64EncodeBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_Base64DecodeBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
     ("BRB_MemBufferKey", None, [ctypes.c_uint, ctypes.c_void_p]),
     ("BRB_MemBufferEncrypt", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_ulong, ctypes.POINTER(ctypes.c_ulong), ctypes.c_uint,
@@ -374,3 +380,29 @@ def membuf_encrypt(buf, size, seed, offset=0, stream=None):
 def membuf_decrypt(buf, size, seed, offset=0, stream=None):
     """BRB_MemBufferDecrypt in place; returns the new MemBuffer size."""
     return _membuf(lib().BRB_MemBufferDecrypt, buf, size, seed, offset, stream)
+
+
+# ---- base64 (SURVEY §8 f4) -------------------------------------------------------------------------
+def base64_encode_batch(data, offsets, lengths, out, out_offsets, stream=None, async_=False):
+    """BRB_Base64EncodeBatch: out[out_offsets[i]:+4*ceil(len/3)] = base64 of record i."""
+    _same_kind(data, offsets, lengths, out, out_offsets)
+    flags, h = _mode(data, stream, async_)
+    _check(lib().BRB_Base64EncodeBatch(_ptr(data), _ptr(offsets), _ptr(lengths), len(offsets), _ptr(out),
+                                       _ptr(out_offsets), flags, h), "BRB_Base64EncodeBatch")
+    return out
+
+
+def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=None, stream=None, async_=False):
+    """BRB_Base64DecodeBatch: returns out_lengths (uint32[n])."""
+    n = len(offsets)
+    if out_lengths is None:
+        if _is_torch(text):
+            import torch
+            out_lengths = torch.zeros(n, dtype=torch.int32, device=text.device)
+        else:
+            out_lengths = np.zeros(n, np.uint32)
+    _same_kind(text, offsets, lengths, out, out_offsets, out_lengths)
+    flags, h = _mode(text, stream, async_)
+    _check(lib().BRB_Base64DecodeBatch(_ptr(text), _ptr(offsets), _ptr(lengths), n, _ptr(out), _ptr(out_offsets),
+                                       _ptr(out_lengths), flags, h), "BRB_Base64DecodeBatch")
+    return out_lengths

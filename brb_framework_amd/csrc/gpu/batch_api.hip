@@ -495,6 +495,57 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
     return rc;
 }
 
+// ---- base64 --------------------------------------------------------------------
+int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, void *out,
+              const uint64_t *ooffs, uint32_t *olens, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n == 0)
+        return BRB_BATCH_OK;
+    if (!in || !offs || !lens || !out || !ooffs || (decode && !olens)) {
+        set_err("NULL data, offsets, lengths, out, out_offsets or out_lengths");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    auto launch = [&](const uint8_t *i, const uint64_t *o, const uint32_t *l, uint8_t *d, const uint64_t *oo,
+                      uint32_t *ol) {
+        return decode ? brb::launch_b64_decode(i, o, l, n, d, oo, ol, s) : brb::launch_b64_encode(i, o, l, n, d, oo, s);
+    };
+    if (flags & BRB_BATCH_DEVICE) {
+        if ((e = launch(static_cast<const uint8_t *>(in), offs, lens, static_cast<uint8_t *>(out), ooffs, olens)) != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    // output extents: encode 4 * ceil(len / 3), decode at most 3 * (len / 4)
+    std::vector<uint32_t> olen_max(n);
+    for (uint64_t i = 0; i < n; i++)
+        olen_max[i] = decode ? 3u * (lens[i] / 4) : 4u * ((lens[i] + 2) / 3);
+    uint64_t lo, hi, olo, ohi;
+    span_of(offs, lens, n, 0, lo, hi);
+    span_of(ooffs, olen_max.data(), n, 0, olo, ohi);
+    const std::vector<uint64_t> roff = rebase(offs, n, lo), rooff = rebase(ooffs, n, olo);
+    Staging st;
+    const size_t i_in = st.add(static_cast<const uint8_t *>(in) + lo, nullptr, size_t(hi - lo));
+    const size_t i_out = st.add(static_cast<uint8_t *>(out) + olo, static_cast<uint8_t *>(out) + olo, size_t(ohi - olo));
+    const size_t i_o = st.add(roff.data(), nullptr, 8 * n);
+    const size_t i_l = st.add(lens, nullptr, 4 * n);
+    const size_t i_oo = st.add(rooff.data(), nullptr, 8 * n);
+    const size_t i_ol = decode ? st.add(nullptr, olens, 4 * n) : 0;
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = launch(st.dev(i_in), reinterpret_cast<const uint64_t *>(st.dev(i_o)), reinterpret_cast<const uint32_t *>(st.dev(i_l)),
+                    st.dev(i_out), reinterpret_cast<const uint64_t *>(st.dev(i_oo)),
+                    decode ? reinterpret_cast<uint32_t *>(st.dev(i_ol)) : nullptr)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
 // ---- MemBuffer Blowfish -------------------------------------------------------
 int membuf_crypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset, unsigned long *new_size,
                  unsigned flags, void *stream, bool decrypt)
@@ -562,6 +613,18 @@ int membuf_crypt(void *buf, unsigned long size, unsigned int seed, unsigned long
 }  // namespace
 
 extern "C" {
+
+int BRB_Base64EncodeBatch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n, void *out,
+                          const uint64_t *out_offsets, unsigned flags, void *hip_stream)
+{
+    return b64_batch(false, data, offsets, lengths, n, out, out_offsets, nullptr, flags, hip_stream);
+}
+
+int BRB_Base64DecodeBatch(const void *text, const uint64_t *offsets, const uint32_t *lengths, uint64_t n, void *out,
+                          const uint64_t *out_offsets, uint32_t *out_lengths, unsigned flags, void *hip_stream)
+{
+    return b64_batch(true, text, offsets, lengths, n, out, out_offsets, out_lengths, flags, hip_stream);
+}
 
 void BRB_MemBufferKey(unsigned int seed, unsigned int key[16])
 {

@@ -24,6 +24,12 @@ hipError_t launch_first_zero_pair(const uint64_t *words, uint64_t n_blocks, unsi
 hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const uint32_t *slen, const uint64_t *first,
                                uint64_t n_rec, uint8_t *out, hipStream_t s);
 
+// base64 (base64_kernels.hip)
+hipError_t launch_b64_encode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
+                             const uint64_t *ooffs, hipStream_t s);
+hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
+                             const uint64_t *ooffs, uint32_t *olens, hipStream_t s);
+
 // RC4 (rc4_kernels.hip): states = n contiguous 264-byte BRB_RC4_State, updated in place
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n, hipStream_t s);

@@ -187,6 +187,22 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
                          const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags,
                          void *hip_stream);
 
+/* ---- base64 -----------------------------------------------------------------------
+ * Encode = brb_base64_encode_to_mb (base64.c:304-361) for n records: record i = data[offsets[i] ..
+ * + lengths[i]) -> out[out_offsets[i] .. + 4 * ceil(lengths[i] / 3)), standard alphabet, '='
+ * padding, no NUL written.  (brb_base64_encode_bin's static 131 070-byte result buffer cap is a
+ * property of that buffer, not of the encoding, and is not reproduced.) */
+int BRB_Base64EncodeBatch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                          void *out, const uint64_t *out_offsets, unsigned flags, void *hip_stream);
+/* Decode = brb_base64_decode_to_mb (base64.c:131-179) for n records: record i = text[offsets[i] ..
+ * + lengths[i]) read as a C string (a NUL ends it); bytes outside the alphabet are skipped, '='
+ * counts as the value 0 (base64.c:374), every 4 counted characters give 3 bytes, a trailing
+ * partial group is dropped.  out_lengths[i] = bytes written at out + out_offsets[i]; the caller
+ * reserves 3 * (lengths[i] / 4) bytes there. */
+int BRB_Base64DecodeBatch(const void *text, const uint64_t *offsets, const uint32_t *lengths, uint64_t n,
+                          void *out, const uint64_t *out_offsets, uint32_t *out_lengths, unsigned flags,
+                          void *hip_stream);
+
 /* ---- MemBuffer Blowfish -------------------------------------------------------
  * MemBufferEncryptData / MemBufferDecryptData (mem_buf.c:1499-1617) on the bytes of a MemBuffer:
  * buf = MemBufferDeref(mb) with mb->offset == 0, size = MemBufferGetSize(mb).  Reproduced exactly:

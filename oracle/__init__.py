@@ -51,6 +51,8 @@ def lib() -> ctypes.CDLL:
             "orc_rc4md5_open": (ctypes.c_int, [vp, vp, u64]),
             "orc_rc4md5_frame_batch": (None, [vp, vp, vp, vp, vp, vp, vp, u64, ctypes.c_int]),
             "orc_rc4md5_open_batch": (None, [vp, vp, vp, vp, u64, vp, ctypes.c_int]),
+            "orc_b64_encode": (u64, [vp, u64, vp]),
+            "orc_b64_decode": (u64, [vp, u64, vp]),
             "orc_splitmix64": (u64, [u64]),
             "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
         }
@@ -213,6 +215,18 @@ def rc4md5_frame_batch(states, payload, offs, lens, salts, frames, foffs, thread
 
 def rc4md5_open_batch(states, frames, offs, lens, valid, threads=1):
     lib().orc_rc4md5_open_batch(_p(states), _p(frames), _p(offs), _p(lens), len(offs), _p(valid), threads)
+
+
+def b64_encode(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(4 * ((len(data) + 2) // 3) + 1)
+    n = lib().orc_b64_encode(bytes(data), len(data), out)
+    return out.raw[:n]
+
+
+def b64_decode(text: bytes) -> bytes:
+    out = ctypes.create_string_buffer(3 * (len(text) // 4) + 1)
+    n = lib().orc_b64_decode(bytes(text), len(text), out)
+    return out.raw[:n]
 
 
 # ---- generator ---------------------------------------------------------------

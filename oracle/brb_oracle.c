@@ -624,6 +624,60 @@ void orc_rc4md5_open_batch(orc_rc4_state *s, uint8_t *frames, const uint64_t *of
 }
 
 /* =========================================================================================== */
+/* base64 -- libbrb_core/crypto/base64.c                                                         */
+/* =========================================================================================== */
+static const char b64_code[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+/* base64.c:304-361: 3 bytes -> 4 characters; a 1- or 2-byte tail is shifted up and padded */
+uint64_t orc_b64_encode(const uint8_t *in, uint64_t len, char *out)
+{
+    uint64_t o = 0, k = 0;
+    for (; k + 3 <= len; k += 3) {
+        uint32_t v = ((uint32_t)in[k] << 16) | ((uint32_t)in[k + 1] << 8) | in[k + 2];
+        out[o++] = b64_code[v >> 18];
+        out[o++] = b64_code[(v >> 12) & 63];
+        out[o++] = b64_code[(v >> 6) & 63];
+        out[o++] = b64_code[v & 63];
+    }
+    uint64_t t = len - k;
+    if (t) {
+        uint32_t v = (uint32_t)in[k] << 16;
+        if (t == 2) v |= (uint32_t)in[k + 1] << 8;
+        out[o++] = b64_code[v >> 18];
+        out[o++] = b64_code[(v >> 12) & 63];
+        out[o++] = t == 2 ? b64_code[(v >> 6) & 63] : '=';
+        out[o++] = '=';
+    }
+    return o;
+}
+
+/* base64.c:363-376 value table: the alphabet, '=' -> 0, everything else -> skipped */
+static int b64_value(unsigned char c)
+{
+    if (c == '=') return 0;
+    const char *p = memchr(b64_code, c, 64);
+    return (c && p) ? (int)(p - b64_code) : -1;
+}
+
+/* base64.c:131-179 */
+uint64_t orc_b64_decode(const char *in, uint64_t len, uint8_t *out)
+{
+    uint64_t o = 0;
+    uint32_t val = 0, c = 0;
+    for (uint64_t k = 0; k < len && in[k]; k++) {
+        int v = b64_value((unsigned char)in[k]);
+        if (v < 0) continue;
+        val = (val << 6) + (uint32_t)v;
+        if (++c < 4) continue;
+        out[o++] = (uint8_t)(val >> 16);
+        out[o++] = (uint8_t)(val >> 8);
+        out[o++] = (uint8_t)val;
+        val = c = 0;
+    }
+    return o;
+}
+
+/* =========================================================================================== */
 /* Generator                                                                                     */
 /* =========================================================================================== */
 uint64_t orc_splitmix64(uint64_t x)

@@ -109,6 +109,14 @@ void orc_rc4md5_frame_batch(orc_rc4_state *s, const uint8_t *payload, const uint
 void orc_rc4md5_open_batch(orc_rc4_state *s, uint8_t *frames, const uint64_t *off, const uint32_t *len, uint64_t n,
                            uint8_t *valid, int n_threads);
 
+/* ---- base64 -- libbrb_core/crypto/base64.c --------------------------------------------------
+ * encode = brb_base64_encode_to_mb (base64.c:304-361): standard alphabet, '=' padding, no cap.
+ * decode = brb_base64_decode_to_mb (:131-179): stops at NUL or after len bytes, skips bytes outside
+ *   the alphabet, '=' counts as value 0 (:363-376), each 4 counted characters give 3 bytes, a
+ *   trailing partial group is dropped.  Both return the output length. */
+uint64_t orc_b64_encode(const uint8_t *in, uint64_t len, char *out);
+uint64_t orc_b64_decode(const char *in, uint64_t len, uint8_t *out);
+
 /* ---- Batches (used by tests and by bench.py's cpu_baseline) ------------------------------- */
 void orc_md5_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out16, int n_threads);
 void orc_sha1_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out20, int n_threads);

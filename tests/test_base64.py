@@ -1,0 +1,99 @@
+"""base64: the oracle against RFC 4648 and Python's base64 (CPU), and the GPU
+batches (BRB_Base64EncodeBatch / BRB_Base64DecodeBatch) against the oracle, bit for bit."""
+import base64
+
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+RFC4648 = [(b"", b""), (b"f", b"Zg=="), (b"fo", b"Zm8="), (b"foo", b"Zm9v"), (b"foob", b"Zm9vYg=="),
+           (b"fooba", b"Zm9vYmE="), (b"foobar", b"Zm9vYmFy")]
+
+
+def test_oracle_rfc4648(orc):
+    for plain, enc in RFC4648:
+        assert orc.b64_encode(plain) == enc
+        # the reference counts '=' as the value 0 (base64.c:374): padding decodes to zero bytes
+        assert orc.b64_decode(enc) == plain + b"\0" * enc.count(b"=")
+
+
+def test_oracle_vs_python(orc):
+    rng = np.random.default_rng(4)
+    for _ in range(200):
+        data = rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes()
+        enc = orc.b64_encode(data)
+        assert enc == base64.b64encode(data)
+        assert orc.b64_decode(enc) == data + b"\0" * enc.count(b"=")
+        # noise outside the alphabet is skipped (base64.c:143-144); a NUL ends the string
+        noisy = b"".join(bytes([c]) + (b"\n" if i % 7 == 0 else b"") for i, c in enumerate(enc))
+        assert orc.b64_decode(noisy) == orc.b64_decode(enc)
+        assert orc.b64_decode(enc[:8] + b"\0" + enc[8:]) == orc.b64_decode(enc[:8])
+
+
+@pytest.fixture(scope="module")
+def torch_dev(brb):
+    import torch
+    assert torch.cuda.is_available(), "no HIP device visible to torch"
+    assert brb.gpu_available(), brb.lib().BRB_CryptoGPU_LastError()
+    return torch
+
+
+def _records(seed, n, max_len):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[: min(n, 30)] = np.arange(min(n, 30))
+    offs, pos = [], 3
+    for L in lens:
+        pos += int(rng.integers(0, 4))
+        offs.append(pos)
+        pos += int(L)
+    return workload.gen_records(0x5EED00B6 + seed, 0, 1, pos + 8), np.array(offs, np.uint64), lens
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,max_len", [(1, 500, 40), (2, 300, 3000), (3, 20, 100000)])
+def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len):
+    data, offs, lens = _records(seed, n, max_len)
+    want = [orc.b64_encode(data[int(o):int(o) + int(L)].tobytes()) for o, L in zip(offs, lens)]
+    elens = np.array([len(w) for w in want], np.uint32)
+    eoffs = np.zeros(n, np.uint64)
+    eoffs[1:] = np.cumsum(elens.astype(np.uint64) + 1)[:-1]      # 1-byte gaps between outputs
+    total = int(eoffs[-1] + elens[-1] + 8)
+    # host mode
+    out = np.full(total, 0xEE, np.uint8)
+    brb.base64_encode_batch(data, offs, lens, out, eoffs)
+    for i in range(n):
+        assert out[int(eoffs[i]):int(eoffs[i]) + int(elens[i])].tobytes() == want[i]
+        assert out[int(eoffs[i]) + int(elens[i])] == 0xEE                  # nothing past the record
+    # device mode
+    t = torch_dev
+    dout = t.full((total,), 0xEE, dtype=t.uint8, device="cuda")
+    brb.base64_encode_batch(t.from_numpy(data).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(), dout,
+                            t.from_numpy(eoffs).cuda())
+    assert np.array_equal(dout.cpu().numpy(), out)
+    # decode the encodings back (with noise bytes and an early NUL in some records)
+    text = out.copy()
+    for i in range(0, n, 5):
+        if elens[i] > 6:
+            text[int(eoffs[i]) + 3] = ord("\n")                 # skipped
+    for i in range(2, n, 11):
+        if elens[i] > 10:
+            text[int(eoffs[i]) + 9] = 0                           # ends the C string
+    dlen_cap = 3 * (elens // 4)
+    doffs = np.zeros(n, np.uint64)
+    doffs[1:] = np.cumsum(dlen_cap.astype(np.uint64))[:-1]
+    dtotal = int(dlen_cap.sum()) + 8
+    hout = np.zeros(dtotal, np.uint8)
+    got_len = brb.base64_decode_batch(text, eoffs, elens, hout, doffs)
+    dd = t.zeros(dtotal, dtype=t.uint8, device="cuda")
+    dl = brb.base64_decode_batch(t.from_numpy(text).cuda(), t.from_numpy(eoffs).cuda(), t.from_numpy(elens).cuda(),
+                                 dd, t.from_numpy(doffs).cuda())
+    dd = dd.cpu().numpy()
+    dl = dl.cpu().numpy()
+    for i in range(n):
+        rec = text[int(eoffs[i]):int(eoffs[i]) + int(elens[i])].tobytes()
+        w = orc.b64_decode(rec)
+        assert int(got_len[i]) == len(w) and int(dl[i]) == len(w), i
+        assert hout[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w
+        assert dd[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w
