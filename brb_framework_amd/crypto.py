@@ -351,9 +351,10 @@ def rc4md5_open_batch(states, frames, offsets, lengths, out=None, valid=None, st
 
 
 # ---- MemBuffer Blowfish ------------------------------------------------------------
-def membuf_span(size: int, offset: int) -> int:
-    """BRB_MEMBUF_SPAN: bytes the call touches after buf + offset."""
-    return (((size + offset) // 8 + 3) // 2) * 16
+def membuf_span(data_size: int) -> int:
+    """BRB_MEMBUF_SPAN: bytes a call touches after buf + offset; data_size = size + offset to
+    encrypt, size - offset to decrypt (mem_buf.c:1503, :1557)."""
+    return ((data_size // 8 + 3) // 2) * 16
 
 
 def membuf_key(seed: int) -> bytes:
@@ -362,8 +363,8 @@ def membuf_key(seed: int) -> bytes:
     return bytes(k)
 
 
-def _membuf(fn, buf, size, seed, offset, stream):
-    need = offset + membuf_span(size, offset)
+def _membuf(fn, buf, size, seed, offset, stream, decrypt):
+    need = offset + membuf_span(size - offset if decrypt else size + offset)
     if _nbytes(buf) < need:
         raise ValueError(f"buffer holds {_nbytes(buf)} bytes, the call needs {need}")
     flags, h = _mode(buf, stream, False)
@@ -374,12 +375,12 @@ def _membuf(fn, buf, size, seed, offset, stream):
 
 def membuf_encrypt(buf, size, seed, offset=0, stream=None):
     """BRB_MemBufferEncrypt in place; returns the new MemBuffer size."""
-    return _membuf(lib().BRB_MemBufferEncrypt, buf, size, seed, offset, stream)
+    return _membuf(lib().BRB_MemBufferEncrypt, buf, size, seed, offset, stream, False)
 
 
 def membuf_decrypt(buf, size, seed, offset=0, stream=None):
     """BRB_MemBufferDecrypt in place; returns the new MemBuffer size."""
-    return _membuf(lib().BRB_MemBufferDecrypt, buf, size, seed, offset, stream)
+    return _membuf(lib().BRB_MemBufferDecrypt, buf, size, seed, offset, stream, True)
 
 
 # ---- base64 (SURVEY §8 f4) -------------------------------------------------------------------------

@@ -95,4 +95,81 @@ struct Snk {
     }
 };
 
+// 64-byte blocks of a byte range at any address, the next block always in flight: a lane that
+// consumes one block per few thousand cycles (RC4, a digest) never waits on HBM latency.  Block b
+// is 16 little-endian chunks, chunk i = range bytes 64 b + 4 i .. + 3; bytes past the range are 0.
+// Loads are aligned-dword based (4 x global_load_dwordx4 at 4-byte alignment for a block that lies
+// inside the range's dwords, guarded single dwords at the end), funnel-shifted with v_alignbit_b32.
+struct BlockSrc {
+    const uint32_t *p;   // dword holding the range's first byte
+    uint32_t sh;         // 8 * (address & 3)
+    uint64_t len, ndw;   // range bytes; dwords holding any of them
+    uint64_t nb;         // block returned by the next fetch()
+    uint32_t prev;       // dword 16 nb (last dword of the previous load)
+    uint32_t L[16];      // dwords 16 nb + 1 .. 16 nb + 16, in flight
+
+    BRB_DEV void load(uint64_t b)
+    {
+        const uint64_t base = 16 * b + 1;
+        if (base + 16 <= ndw) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint4 v = ld16_a4(reinterpret_cast<const uint8_t *>(p + base + 4 * q));
+                L[4 * q + 0] = v.x;
+                L[4 * q + 1] = v.y;
+                L[4 * q + 2] = v.z;
+                L[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                L[i] = base + i < ndw ? p[base + i] : 0u;
+        }
+    }
+
+    BRB_DEV void init(const uint8_t *a, uint64_t n)
+    {
+        const uintptr_t ad = reinterpret_cast<uintptr_t>(a);
+        p = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
+        sh = uint32_t(ad & 3) * 8;
+        len = n;
+        ndw = n ? ((ad & 3) + n + 3) / 4 : 0;
+        prev = ndw ? p[0] : 0u;
+        nb = 0;
+        load(0);
+    }
+
+    // chunks of block nb; starts the load of block nb + 1
+    BRB_DEV void fetch(uint32_t (&c)[16])
+    {
+        uint32_t cur[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            cur[i] = L[i];
+        load(nb + 1);
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            c[i] = __builtin_amdgcn_alignbit(cur[i], i ? cur[i - 1] : prev, sh);
+        prev = cur[15];
+        const uint64_t pos = 64 * nb;
+        if (pos + 64 > len) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t q = pos + 4 * i;
+                c[i] = q >= len ? 0u : q + 4 <= len ? c[i] : c[i] & ((1u << (8 * uint32_t(len - q))) - 1u);
+            }
+        }
+        ++nb;
+    }
+};
+
+// The 0x80 end marker of MD5 / SHA-1 padding at byte len % 64 of a (zero-filled) tail block.
+BRB_DEV void add_marker(uint32_t (&w)[16], uint64_t len)
+{
+    const uint32_t t = uint32_t(len & 63), m = 0x80u << (8 * (t & 3));
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+        w[i] |= i == (t >> 2) ? m : 0u;
+}
+
 }  // namespace brb_io

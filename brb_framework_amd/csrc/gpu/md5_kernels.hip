@@ -5,6 +5,7 @@
 // one-block software prefetch; the record's 16 message words are consumed straight from VGPRs.
 // Digest of record r = BRB_MD5Init + BRB_MD5Update(record) + BRB_MD5Final (md5.c:38-168).
 #include "brb_kernels.h"
+#include "byte_stream.h"
 #include "digest_dma.h"
 #include "md5_device.h"
 
@@ -86,15 +87,14 @@ __global__ __launch_bounds__(BLOCK) void md5_any_kernel(const uint8_t *__restric
     const uint64_t nfull = len >> 6;
     Md5State st = md5_iv();
     uint32_t w[16];
+    brb_io::BlockSrc src;           // the next 64-byte block is always in flight
+    src.init(a, len);
     for (uint64_t b = 0; b < nfull; ++b) {
-#pragma unroll
-        for (uint32_t i = 0; i < 16; i++)
-            w[i] = word_any(a, len, 64 * b, i);
+        src.fetch(w);
         md5_compress(st, w);
     }
-#pragma unroll
-    for (uint32_t i = 0; i < 16; i++)
-        w[i] = word_any(a, len, 64 * nfull, i);
+    src.fetch(w);                   // tail (bytes past the record read as 0)
+    brb_io::add_marker(w, len);
     md5_finish(st, w, uint32_t(len & 63), len);
     Out16::store<OUT_ALIGNED>(out, r, st);
 }

@@ -21,6 +21,31 @@ constexpr int kWave = 64;
 
 BRB_DEV uint32_t clamp4(uint64_t left) { return left >= 4 ? 4u : uint32_t(left); }
 
+// Decrypt frame block b (chunks 16b .. 16b + 15 of a frame of F bytes) into pt and the sink.
+BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, uint64_t b, uint32_t (&pt)[16])
+{
+    uint32_t c[16];
+    src.fetch(c);
+    const uint64_t pos = 64 * b;
+    if (pos + 64 <= F) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            pt[i] = c[i] ^ g.next4();
+            snk.put(pt[i]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint64_t q = pos + 4 * i;
+            pt[i] = 0;
+            if (q < F) {
+                pt[i] = c[i] ^ g.next_n(clamp4(F - q));
+                snk.put(pt[i]);
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
                                                           const uint32_t *__restrict__ lens, uint64_t n)
@@ -35,18 +60,27 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
     g.P.lb = lane * 4;
     g.load(states + s * kStateBytes);
     const uint64_t off = offs[s], len = lens[s];
-    Src src;
+    brb_io::BlockSrc src;
     Snk snk;
     src.init(in + off, len);
     snk.init(out + off, len);
-    const uint64_t full = len >> 2;
-    for (uint64_t c = 0; c < full; c++) {
-        const uint32_t v = src.next();
-        snk.put(v ^ g.next4());
-    }
-    if (len & 3) {
-        const uint32_t v = src.next();
-        snk.put(v ^ g.next_n(uint32_t(len & 3)));
+    const uint64_t nblk = (len + 63) >> 6;
+    for (uint64_t b = 0; b < nblk; b++) {
+        uint32_t c[16];
+        src.fetch(c);
+        const uint64_t pos = 64 * b;
+        if (pos + 64 <= len) {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                snk.put(c[i] ^ g.next4());
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t q = pos + 4 * i;
+                if (q < len)
+                    snk.put(c[i] ^ g.next_n(clamp4(len - q)));
+            }
+        }
     }
     snk.flush();
     g.store(states + s * kStateBytes);
@@ -78,7 +112,7 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
         kh[k] = g.next4();
     kh[7] = g.next_n(clamp4(F - 28));
 
-    Src src;
+    brb_io::BlockSrc src;
     src.init(payload + offs[s], len);
     Snk snk;                                      // frame bytes 32..F-1
     snk.init(frame + 32, F > 32 ? F - 32 : 0);
@@ -86,11 +120,12 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
     const uint64_t nblk = md5_blocks(len), nw = 16 * nblk;
     uint32_t prev = 0, first = 0;
     for (uint64_t b = 0; b < nblk; b++) {
-        uint32_t m[16];
+        uint32_t m[16], rw[16];
+        src.fetch(rw);
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++) {
             const uint64_t w = 16 * b + i;
-            const uint32_t raw = src.next();
+            const uint32_t raw = rw[i];
             if (w == 0) {
                 first = raw;
             } else {
@@ -141,50 +176,39 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     g.P.lb = lane * 4;
     g.load(states + s * kStateBytes);
     const uint64_t off = offs[s], F = lens[s];
-    Src src;
+    brb_io::BlockSrc src;
     Snk snk;
     src.init(in + off, F);
     snk.init(out + off, F);
 
-    // header chunks 0..7 (frame bytes 0..31)
-    uint32_t hd[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint64_t fb = 4 * uint64_t(k);
-        const uint32_t nb = fb < F ? clamp4(F - fb) : 0u;
-        const uint32_t raw = src.next();
-        hd[k] = raw ^ (nb ? g.next_n(nb) : 0u);
-        snk.put(hd[k]);
-    }
-
+    // frame block 0 = chunks 0..15; the header is chunks 0..7 (frame bytes 0..31)
+    uint32_t cur[16];
+    decrypt_block(src, snk, g, F, 0, cur);
     uint32_t ok = 0;
     if (F >= kHeader) {
-        // payload word w = frame bytes 30 + 4w .. 33 + 4w = chunks w + 7 (high half) and w + 8 (low half)
+        // payload word w = frame bytes 30 + 4w .. 33 + 4w: the high half of chunk w + 7 and the low
+        // half of chunk w + 8; MD5 block b needs chunks 16b + 7 .. 16b + 23 = frame blocks b, b + 1
         const uint64_t len = F - kHeader;
         const uint64_t nblk = md5_blocks(len), nw = 16 * nblk;
+        const uint32_t h2 = cur[2], h3 = cur[3], h4 = cur[4], h5 = cur[5], h6 = cur[6], h7 = cur[7];
         Md5State st = md5_iv();
-        uint32_t prev = hd[7];
         for (uint64_t b = 0; b < nblk; b++) {
-            uint32_t m[16];
+            uint32_t nxt[16], m[16];
+            decrypt_block(src, snk, g, F, b + 1, nxt);
 #pragma unroll
-            for (uint32_t i = 0; i < 16; i++) {
-                const uint64_t w = 16 * b + i;
-                const uint64_t fb = 4 * (w + 8);
-                uint32_t pt = 0;
-                if (fb < F) {
-                    pt = src.next() ^ g.next_n(clamp4(F - fb));
-                    snk.put(pt);
-                }
-                m[i] = md5_pad_word(__builtin_amdgcn_alignbit(pt, prev, 16), w, len, nw);
-                prev = pt;
+            for (int i = 0; i < 16; i++) {
+                const uint32_t lo = i + 7 < 16 ? cur[i + 7] : nxt[i - 9];
+                const uint32_t hi = i + 8 < 16 ? cur[i + 8] : nxt[i - 8];
+                m[i] = md5_pad_word(__builtin_amdgcn_alignbit(hi, lo, 16), 16 * b + i, len, nw);
             }
             md5_compress(st, m);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                cur[i] = nxt[i];
         }
-        const bool tag = hd[2] == 0x48534148u && (hd[3] & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
-        const bool dig = __builtin_amdgcn_alignbit(hd[4], hd[3], 8) == st.a &&
-                         __builtin_amdgcn_alignbit(hd[5], hd[4], 8) == st.b &&
-                         __builtin_amdgcn_alignbit(hd[6], hd[5], 8) == st.c &&
-                         __builtin_amdgcn_alignbit(hd[7], hd[6], 8) == st.d;
+        const bool tag = h2 == 0x48534148u && (h3 & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
+        const bool dig = __builtin_amdgcn_alignbit(h4, h3, 8) == st.a && __builtin_amdgcn_alignbit(h5, h4, 8) == st.b &&
+                         __builtin_amdgcn_alignbit(h6, h5, 8) == st.c && __builtin_amdgcn_alignbit(h7, h6, 8) == st.d;
         ok = tag && dig;
     }
     snk.flush();

@@ -2,6 +2,7 @@
 // Digest of record r = BrbSha1_Do(record) (libbrb_core/crypto/sha1.c:203-216): 20 raw bytes,
 // big-endian state words (sha1.c:185-188).
 #include "brb_kernels.h"
+#include "byte_stream.h"
 #include "digest_dma.h"
 #include "sha1_device.h"
 
@@ -91,15 +92,17 @@ __global__ __launch_bounds__(BLOCK) void sha1_any_kernel(const uint8_t *__restri
     const uint64_t nfull = len >> 6;
     Sha1State st = sha1_iv();
     uint32_t w[16];
+    brb_io::BlockSrc src;           // the next 64-byte block is always in flight
+    src.init(a, len);
     for (uint64_t b = 0; b < nfull; ++b) {
+        src.fetch(w);
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++)
-            w[i] = __builtin_bswap32(word_any(a, len, 64 * b, i));
+            w[i] = __builtin_bswap32(w[i]);
         sha1_compress(st, w);
     }
-#pragma unroll
-    for (uint32_t i = 0; i < 16; i++)
-        w[i] = word_any(a, len, 64 * nfull, i);
+    src.fetch(w);                   // tail (bytes past the record read as 0)
+    brb_io::add_marker(w, len);
     sha1_finish(st, w, uint32_t(len & 63), len);
     store20<OUT_ALIGNED>(out, r, st);
 }

@@ -213,10 +213,11 @@ int BRB_Base64DecodeBatch(const void *text, const uint64_t *offsets, const uint3
  *            holding a zero word; new size = 8 * words decrypted + offset
  * (so decrypt(encrypt(x)) does not restore x, as in the reference).  The caller grows the buffer
  * first, as MemBufferCheckForGrow does (mem_buf.c:1525, 1585): buf must hold
- * offset + BRB_MEMBUF_SPAN(size, offset) bytes.  The Blowfish context is built on the host; the
+ * offset + BRB_MEMBUF_SPAN(size + offset) bytes to encrypt, offset + BRB_MEMBUF_SPAN(size - offset)
+ * bytes to decrypt.  The Blowfish context is built on the host; the
  * ECB pass (and the zero-pair scan) run on the GPU.  Device mode needs buf + offset 8-byte
  * aligned.  Both calls return when *new_size is known (ASYNC is ignored). */
-#define BRB_MEMBUF_SPAN(size, offset) (((((size) + (offset)) / 8 + 3) / 2) * 16)
+#define BRB_MEMBUF_SPAN(data_size) ((((data_size) / 8 + 3) / 2) * 16)
 void BRB_MemBufferKey(unsigned int seed, unsigned int key[16]);
 int BRB_MemBufferEncrypt(void *buf, unsigned long size, unsigned int seed, unsigned long offset,
                          unsigned long *new_size, unsigned flags, void *hip_stream);
