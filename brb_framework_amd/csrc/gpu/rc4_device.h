@@ -1,15 +1,16 @@
 // rc4_device.h -- device code of the batched RC4 and RC4+MD5 framing kernels.
 //
 // RC4 (libbrb_core/crypto/rc4.c:64-87) is a byte-serial chain over a 256-byte permutation that
-// every byte mutates, so the parallelism is across connections: one lane owns one stream, and the
-// 64 lanes of a wave keep their 64 permutations in one 16 KiB LDS slot laid out so that every access
-// of lane l lands in bank l, whatever the index:
+// every byte mutates, so the parallelism is across connections: one lane owns one stream.  A
+// workgroup of 4 waves keeps its 256 permutations in one 64 KiB LDS image laid out so that every
+// access of lane l lands in bank l, whatever the index, and costs one VALU op to address:
 //
-//   byte x of lane l's permutation  ->  LDS byte (x >> 2) * 256 + l * 4 + (x & 3)
+//   byte x of the permutation of (wave w, lane l)  ->  LDS byte  x * 256 + l * 4 + w
 //
-// (64 rows of one dword per lane).  Random indices therefore never conflict.  Per keystream byte:
-// S[j] is the only read on the dependency chain; S[i + 1] is read ahead before the swap is written
-// and patched when the swap moved it (j == i + 1); S[S[i] + S[j]] is read after the swap.
+// (256 rows, one dword per lane, one byte of it per wave).  Random indices never conflict, and an
+// address is a single v_lshl_or_b32 of the 8-bit index.  Per keystream byte: S[j] is the only read
+// on the dependency chain; S[i + 1] is read ahead before the swap is written and patched when the
+// swap moved it (j == i + 1); S[S[i] + S[j]] is read after the swap.
 //
 // Memory side: byte_stream.h (aligned-dword Src / Snk for streams at arbitrary byte offsets).
 #pragma once
@@ -24,17 +25,17 @@ using brb_io::Snk;
 using brb_io::Src;
 
 constexpr uint32_t kStateBytes = 264;   // sizeof(BRB_RC4_State), libbrb_data.h:887-897
-constexpr uint32_t kWaveLds = 16384;    // 64 lanes x 256-byte permutation
+constexpr uint32_t kWaves = 4;          // waves per workgroup
+constexpr uint32_t kSlotLds = 65536;    // 256 rows x 64 lanes x 4 waves
 constexpr uint32_t kHeader = 30;        // salt(8) "HASH:"(5) MD5(16) NUL(1), ev_kq_aio_transform.c:224-227
 
 struct Perm {
-    uint8_t *lds;   // the wave's 16 KiB slot
-    uint32_t lb;    // lane * 4
+    uint8_t *lds;   // the workgroup's 64 KiB image
+    uint32_t lw;    // lane * 4 + wave
 
-    BRB_DEV uint32_t addr(uint32_t x) const { return ((x << 6) & 0x3F00u) | (x & 3u) | lb; }
+    BRB_DEV uint32_t addr(uint32_t x) const { return (x << 8) | lw; }
     BRB_DEV uint32_t rd(uint32_t x) const { return lds[addr(x)]; }
     BRB_DEV void wr(uint32_t x, uint32_t v) const { lds[addr(x)] = uint8_t(v); }
-    BRB_DEV uint32_t &row(uint32_t k) const { return *reinterpret_cast<uint32_t *>(lds + (k << 8) + lb); }
 };
 
 // Keystream generator: BRB_RC4_Crypt's index1/index2 walk (rc4.c:71-82).
@@ -44,13 +45,17 @@ struct Gen {
     uint32_t si;     // S[(i + 1) & 255], read ahead
     uint32_t tail;   // dword 64 of the state: index1, index2 and the two bytes after them
 
-    // BRB_RC4_State (4-byte aligned) -> LDS slot + registers
+    // BRB_RC4_State (4-byte aligned) -> LDS image + registers
     BRB_DEV void load(const uint8_t *st)
     {
         const uint32_t *w = reinterpret_cast<const uint32_t *>(st);
 #pragma unroll 8
-        for (uint32_t k = 0; k < 64; k++)
-            P.row(k) = w[k];
+        for (uint32_t k = 0; k < 64; k++) {
+            const uint32_t v = w[k];
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+                P.wr(4 * k + b, v >> (8 * b));
+        }
         tail = w[64];
         i = tail & 255u;
         j = (tail >> 8) & 255u;
@@ -62,7 +67,7 @@ struct Gen {
         uint32_t *w = reinterpret_cast<uint32_t *>(st);
 #pragma unroll 8
         for (uint32_t k = 0; k < 64; k++)
-            w[k] = P.row(k);
+            w[k] = P.rd(4 * k) | (P.rd(4 * k + 1) << 8) | (P.rd(4 * k + 2) << 16) | (P.rd(4 * k + 3) << 24);
         w[64] = (tail & 0xFFFF0000u) | (j << 8) | i;
     }
 

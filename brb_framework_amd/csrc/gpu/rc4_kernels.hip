@@ -1,7 +1,7 @@
 // rc4_kernels.hip -- batched RC4 and RC4+MD5 framing for gfx950.
 //
-// One lane per connection stream, one wave per workgroup, the wave's 64 permutations in a 16 KiB
-// LDS slot (rc4_device.h).  Lanes touch only their own LDS bytes, so no barrier is needed.
+// One lane per connection stream, 4 waves per workgroup, the workgroup's 256 permutations in a
+// 64 KiB LDS image (rc4_device.h).  Lanes touch only their own LDS bytes, so no barrier is needed.
 //
 //   rc4_crypt_kernel   BRB_RC4_Crypt on every stream                          (rc4.c:64-87)
 //   rc4md5_frame_kernel  WRITE side of EvAIOReqTransform_CryptoRaw(RC4_MD5):  one pass over the
@@ -17,7 +17,7 @@ namespace {
 
 using namespace brb_rc4;
 
-constexpr int kWave = 64;
+constexpr int kWave = 64 * int(kWaves);   // threads per workgroup
 
 BRB_DEV uint32_t clamp4(uint64_t left) { return left >= 4 ? 4u : uint32_t(left); }
 
@@ -50,14 +50,13 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
                                                           const uint64_t *__restrict__ offs,
                                                           const uint32_t *__restrict__ lens, uint64_t n)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t slot[kWaveLds];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t s = uint64_t(blockIdx.x) * kWave + lane;
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
     if (s >= n)
         return;
     Gen g;
     g.P.lds = slot;
-    g.P.lb = lane * 4;
+    g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
     g.load(states + s * kStateBytes);
     const uint64_t off = offs[s], len = lens[s];
     brb_io::BlockSrc src;
@@ -92,14 +91,13 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
                                                              const uint64_t *__restrict__ salts, uint8_t *frames,
                                                              const uint64_t *__restrict__ foffs, uint64_t n)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t slot[kWaveLds];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t s = uint64_t(blockIdx.x) * kWave + lane;
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
     if (s >= n)
         return;
     Gen g;
     g.P.lds = slot;
-    g.P.lb = lane * 4;
+    g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
     g.load(states + s * kStateBytes);
     const uint64_t len = lens[s];
     const uint64_t F = kHeader + len;            // frame bytes
@@ -166,14 +164,13 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint8_t *__restrict__ valid)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t slot[kWaveLds];
-    const uint32_t lane = threadIdx.x;
-    const uint64_t s = uint64_t(blockIdx.x) * kWave + lane;
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
     if (s >= n)
         return;
     Gen g;
     g.P.lds = slot;
-    g.P.lb = lane * 4;
+    g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
     g.load(states + s * kStateBytes);
     const uint64_t off = offs[s], F = lens[s];
     brb_io::BlockSrc src;
