@@ -22,6 +22,11 @@ from .crypto import (  # noqa: F401
     RC4MD5_HEADER,
     BrbSha1Ctx,
     LIB_PATH,
+    CRYPTO_FUNC_RC4,
+    CRYPTO_FUNC_RC4_MD5,
+    OP_READ,
+    OP_WRITE,
+    TransformBatcher,
     base64_decode_batch,
     base64_encode_batch,
     blowfish_ctx_bytes,
@@ -55,5 +60,5 @@ __all__ = [
     "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
     "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "base64_decode_batch",
-    "base64_encode_batch",
+    "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
 ]

@@ -111,6 +111,15 @@ _SIGNATURES = [
     ("BRB_MemBufferDecrypt", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_uint, ctypes.c_ulong, ctypes.POINTER(ctypes.c_ulong), ctypes.c_uint,
       ctypes.c_void_p]),
+    ("BRB_TransformBatcherCreate", ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int]),
+    ("BRB_TransformBatcherDestroy", None, [ctypes.c_void_p]),
+    ("BRB_TransformBatcherEnable", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]),
+    ("BRB_TransformBatcherRead", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]),
+    ("BRB_TransformBatcherWrite", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
+    ("BRB_TransformBatcherFlush", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("BRB_TransformBatcherGetState", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(BRB_RC4_State)]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
@@ -407,3 +416,55 @@ def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=No
     _check(lib().BRB_Base64DecodeBatch(_ptr(text), _ptr(offsets), _ptr(lengths), n, _ptr(out), _ptr(out_offsets),
                                        _ptr(out_lengths), flags, h), "BRB_Base64DecodeBatch")
     return out_lengths
+
+
+# ---- receive-loop batching ---------------------------------------------------------
+CRYPTO_FUNC_RC4, CRYPTO_FUNC_RC4_MD5 = 1, 2
+OP_READ, OP_WRITE = 0, 1
+TransformDone = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
+                                 ctypes.c_int)
+
+
+class TransformBatcher:
+    """BRB_TransformBatcher*: one event-loop round of many connections per GPU call."""
+
+    def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5):
+        self._L = lib()
+        self.h = self._L.BRB_TransformBatcherCreate(max_conns, max_round_bytes, algo)
+        if not self.h:
+            raise RuntimeError("BRB_TransformBatcherCreate: " + self._L.BRB_CryptoGPU_LastError().decode())
+
+    def close(self):
+        if self.h:
+            self._L.BRB_TransformBatcherDestroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def enable(self, conn: int, key: bytes):
+        _check(self._L.BRB_TransformBatcherEnable(self.h, conn, bytes(key), len(key)), "BRB_TransformBatcherEnable")
+
+    def read(self, conn: int, data: bytes) -> int:
+        return self._L.BRB_TransformBatcherRead(self.h, conn, bytes(data), len(data))
+
+    def write(self, conn: int, data: bytes, salt: int) -> int:
+        return self._L.BRB_TransformBatcherWrite(self.h, conn, bytes(data), len(data), salt)
+
+    def flush(self):
+        """Returns [(conn, op, out bytes, valid)] in submission order."""
+        res = []
+
+        def cb(_user, conn, op, out, n, valid):
+            res.append((conn, op, ctypes.string_at(out, n) if n else b"", valid))
+
+        fn = TransformDone(cb)
+        rc = self._L.BRB_TransformBatcherFlush(self.h, fn, None)
+        if rc < 0 or (rc == 0 and self._L.BRB_CryptoGPU_LastError()):
+            raise RuntimeError("BRB_TransformBatcherFlush: " + self._L.BRB_CryptoGPU_LastError().decode())
+        return res
+
+    def state(self, conn: int, op: int) -> bytes:
+        st = BRB_RC4_State()
+        _check(self._L.BRB_TransformBatcherGetState(self.h, conn, op, ctypes.byref(st)), "BRB_TransformBatcherGetState")
+        return rc4_state_bytes(st)

@@ -15,11 +15,17 @@
 #include <vector>
 
 #include "brb_crypto.h"
+#include "api_util.h"
 #include "brb_kernels.h"
 
-namespace {
+namespace brb_api {
 
 thread_local std::string t_err;
+
+void clear_err()
+{
+    t_err.clear();
+}
 
 void set_err(const char *fmt, ...)
 {
@@ -49,6 +55,15 @@ int device_ok()
     }
     return BRB_BATCH_OK;
 }
+
+}  // namespace brb_api
+
+namespace {
+
+using brb_api::device_ok;
+using brb_api::fail_hip;
+using brb_api::set_err;
+using brb_api::t_err;
 
 // Per-thread, per-device grow-only scratch for host-mode batches.
 struct Workspace {

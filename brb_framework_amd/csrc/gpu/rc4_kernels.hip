@@ -48,7 +48,8 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
 
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
-                                                          const uint32_t *__restrict__ lens, uint64_t n)
+                                                          const uint32_t *__restrict__ lens, uint64_t n,
+                                                          const uint32_t *__restrict__ sidx)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
@@ -57,7 +58,8 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
     Gen g;
     g.P.lds = slot;
     g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
-    g.load(states + s * kStateBytes);
+    uint8_t *state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;   // sidx: connection table
+    g.load(state);
     const uint64_t off = offs[s], len = lens[s];
     brb_io::BlockSrc src;
     Snk snk;
@@ -82,14 +84,15 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
         }
     }
     snk.flush();
-    g.store(states + s * kStateBytes);
+    g.store(state);
 }
 
 __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict__ states, const uint8_t *__restrict__ payload,
                                                              const uint64_t *__restrict__ offs,
                                                              const uint32_t *__restrict__ lens,
                                                              const uint64_t *__restrict__ salts, uint8_t *frames,
-                                                             const uint64_t *__restrict__ foffs, uint64_t n)
+                                                             const uint64_t *__restrict__ foffs, uint64_t n,
+                                                             const uint32_t *__restrict__ sidx)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
@@ -98,7 +101,8 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
     Gen g;
     g.P.lds = slot;
     g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
-    g.load(states + s * kStateBytes);
+    uint8_t *state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;   // sidx: connection table
+    g.load(state);
     const uint64_t len = lens[s];
     const uint64_t F = kHeader + len;            // frame bytes
     uint8_t *frame = frames + foffs[s];
@@ -156,13 +160,14 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
     for (int k = 0; k < 8; k++)
         hs.put(h[k] ^ kh[k]);
     hs.flush();
-    g.store(states + s * kStateBytes);
+    g.store(state);
 }
 
 __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                             const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint8_t *__restrict__ valid)
+                                                            uint8_t *__restrict__ valid,
+                                                            const uint32_t *__restrict__ sidx)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
@@ -171,7 +176,8 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     Gen g;
     g.P.lds = slot;
     g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
-    g.load(states + s * kStateBytes);
+    uint8_t *state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;   // sidx: connection table
+    g.load(state);
     const uint64_t off = offs[s], F = lens[s];
     brb_io::BlockSrc src;
     Snk snk;
@@ -210,7 +216,7 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     }
     snk.flush();
     valid[s] = uint8_t(ok);
-    g.store(states + s * kStateBytes);
+    g.store(state);
 }
 
 inline unsigned grid_for(uint64_t n) { return unsigned((n + kWave - 1) / kWave); }
@@ -220,30 +226,30 @@ inline unsigned grid_for(uint64_t n) { return unsigned((n + kWave - 1) / kWave);
 namespace brb {
 
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
-                            const uint32_t *lens, uint64_t n, hipStream_t s)
+                            const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx)
 {
     if (n == 0)
         return hipSuccess;
-    rc4_crypt_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n);
+    rc4_crypt_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx);
     return hipGetLastError();
 }
 
 hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const uint64_t *offs, const uint32_t *lens,
                                const uint64_t *salts, uint8_t *frames, const uint64_t *foffs, uint64_t n,
-                               hipStream_t s)
+                               hipStream_t s, const uint32_t *sidx)
 {
     if (n == 0)
         return hipSuccess;
-    rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n);
+    rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n, sidx);
     return hipGetLastError();
 }
 
 hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
-                              const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s)
+                              const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s, const uint32_t *sidx)
 {
     if (n == 0)
         return hipSuccess;
-    rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid);
+    rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx);
     return hipGetLastError();
 }
 

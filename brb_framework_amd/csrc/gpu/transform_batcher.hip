@@ -1,0 +1,317 @@
+// transform_batcher.hip -- receive-loop batching of the comm transform.
+//
+// The reference calls the transform hook per buffer on the connection's event thread
+// (EvAIOReqTransform_ReadData / _WriteData, ev_kq_aio_transform.c:42-70).  The batcher collects the
+// buffers of one event-loop round from many connections in a pinned host arena, runs the round as
+// one H2D copy, one kernel per direction and sub-round, one D2H copy, and hands every result back
+// in submission order.  The connections' RC4 states (CommEvCryptoInfo's read and write
+// BRB_RC4_State, libbrb_ev_comm.h:206-236) stay resident in HBM; the kernels address them through a
+// connection table (launch_rc4_* `sidx`).
+//
+// Ordering: a connection's buffers in one direction form one RC4 stream, so a round may hold at
+// most one of them per sub-round; the k-th buffer of a connection in a round runs in sub-round k.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "api_util.h"
+#include "brb_crypto.h"
+#include "brb_kernels.h"
+
+using brb_api::fail_hip;
+using brb_api::set_err;
+
+namespace {
+
+constexpr uint32_t kHdr = BRB_RC4MD5_HEADER;
+constexpr size_t kAlign = 256;    // arenas
+constexpr size_t kMetaItem = 80;  // metadata bytes budgeted per buffer: 32 of arrays + up to 40 of padding + valid
+
+inline size_t up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Item {
+    uint32_t conn;
+    int op;
+    uint64_t in_off;
+    uint32_t in_len;
+    uint64_t out_off;
+    uint32_t out_len;
+    uint64_t salt;
+    uint32_t round;   // sub-round
+};
+
+}  // namespace
+
+struct BRB_TransformBatcher {
+    uint32_t max_conns = 0;
+    uint64_t cap = 0;          // input bytes per round
+    int algo = 0;
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    uint8_t *d_states = nullptr;           // [2][max_conns] x 264 B: read states, then write states
+    uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr;   // pinned
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr;
+    size_t out_cap = 0, meta_cap = 0;
+    uint64_t max_items = 0;    // buffers per round: 4 per connection on average
+    uint64_t in_used = 0, out_used = 0;
+    std::vector<Item> items;
+    std::vector<uint8_t> enabled;
+
+    ~BRB_TransformBatcher()
+    {
+        (void)hipSetDevice(dev);
+        if (stream)
+            (void)hipStreamSynchronize(stream);
+        (void)hipFree(d_states);
+        (void)hipFree(d_in);
+        (void)hipFree(d_out);
+        (void)hipFree(d_meta);
+        (void)hipHostFree(h_in);
+        (void)hipHostFree(h_out);
+        (void)hipHostFree(h_meta);
+        if (stream)
+            (void)hipStreamDestroy(stream);
+    }
+
+    uint8_t *state(uint32_t conn, int op) { return d_states + (size_t(op) * max_conns + conn) * sizeof(BRB_RC4_State); }
+};
+
+extern "C" {
+
+BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t max_round_bytes, int algo)
+{
+    brb_api::clear_err();
+    if (max_conns == 0 || max_round_bytes == 0 || (algo != BRB_CRYPTO_FUNC_RC4 && algo != BRB_CRYPTO_FUNC_RC4_MD5)) {
+        set_err("max_conns and max_round_bytes must be > 0 and algo RC4 (1) or RC4_MD5 (2)");
+        return nullptr;
+    }
+    if (brb_api::device_ok() != BRB_BATCH_OK)
+        return nullptr;
+    auto *b = new BRB_TransformBatcher;
+    b->max_conns = max_conns;
+    b->cap = max_round_bytes;
+    b->algo = algo;
+    b->enabled.assign(max_conns, 0);
+    // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
+    b->max_items = 4 * uint64_t(max_conns);
+    b->out_cap = up(max_round_bytes + kHdr * b->max_items, kAlign);
+    b->meta_cap = up(kMetaItem * b->max_items + 4096, kAlign);
+    hipError_t e;
+    if ((e = hipGetDevice(&b->dev)) != hipSuccess || (e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc(&b->d_states, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
+        (e = hipMemset(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
+        (e = hipMalloc(&b->d_in, up(max_round_bytes, kAlign))) != hipSuccess ||
+        (e = hipMalloc(&b->d_out, b->out_cap)) != hipSuccess || (e = hipMalloc(&b->d_meta, b->meta_cap)) != hipSuccess ||
+        (e = hipHostMalloc(&b->h_in, up(max_round_bytes, kAlign), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&b->h_out, b->out_cap, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&b->h_meta, b->meta_cap, hipHostMallocDefault)) != hipSuccess) {
+        fail_hip("transform batcher allocation", e);
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+void BRB_TransformBatcherDestroy(BRB_TransformBatcher *b)
+{
+    delete b;
+}
+
+int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const void *key, int key_sz)
+{
+    brb_api::clear_err();
+    if (!b || !key || key_sz <= 0 || conn >= b->max_conns) {
+        set_err("bad batcher, key or connection id");
+        return BRB_BATCH_BADARG;
+    }
+    BRB_RC4_State st;
+    memset(&st, 0, sizeof(st));              // ev_kq_aio_transform.c:78 memset of the crypto states
+    BRB_RC4_Init(&st, static_cast<const unsigned char *>(key), key_sz);
+    hipError_t e;
+    for (int op = 0; op < 2; op++)
+        if ((e = hipMemcpyAsync(b->state(conn, op), &st, sizeof(st), hipMemcpyHostToDevice, b->stream)) != hipSuccess)
+            return fail_hip("hipMemcpyAsync H2D", e);
+    if ((e = hipStreamSynchronize(b->stream)) != hipSuccess)
+        return fail_hip("hipStreamSynchronize", e);
+    b->enabled[conn] = 1;
+    return BRB_BATCH_OK;
+}
+
+static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *data, uint32_t len, uint64_t salt)
+{
+    brb_api::clear_err();
+    if (!b || (!data && len) || conn >= b->max_conns || !b->enabled[conn]) {
+        set_err("bad batcher, data or connection (not enabled?)");
+        return BRB_BATCH_BADARG;
+    }
+    const uint32_t out_len = len + (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 && op == BRB_CRYPTO_OP_WRITE ? kHdr : 0);
+    const size_t meta_need = kMetaItem * (b->items.size() + 1) + 4096;
+    if (b->items.size() >= b->max_items || b->in_used + len > b->cap || b->out_used + out_len > b->out_cap ||
+        meta_need > b->meta_cap) {
+        set_err("round is full: flush first");
+        return BRB_BATCH_NOT_DONE;
+    }
+    Item it{conn, op, b->in_used, len, b->out_used, out_len, salt, 0};
+    if (len)
+        memcpy(b->h_in + b->in_used, data, len);
+    b->in_used += len;
+    b->out_used += out_len;
+    b->items.push_back(it);
+    return BRB_BATCH_OK;
+}
+
+int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len)
+{
+    return submit(b, conn, BRB_CRYPTO_OP_READ, data, len, 0);
+}
+
+int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt)
+{
+    return submit(b, conn, BRB_CRYPTO_OP_WRITE, data, len, salt);
+}
+
+int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
+{
+    brb_api::clear_err();
+    if (!b) {
+        set_err("NULL batcher");
+        return BRB_BATCH_BADARG;
+    }
+    const size_t n = b->items.size();
+    if (n == 0)
+        return 0;
+    hipError_t e;
+    if ((e = hipSetDevice(b->dev)) != hipSuccess)
+        return fail_hip("hipSetDevice", e);
+    // sub-round of every item: its rank among the same connection's items in the same direction
+    std::vector<uint32_t> seen(size_t(2) * b->max_conns, 0);
+    uint32_t rounds = 0;
+    for (Item &it : b->items) {
+        it.round = seen[size_t(it.op) * b->max_conns + it.conn]++;
+        rounds = std::max(rounds, it.round + 1);
+    }
+    // metadata: per (sub-round, op) a contiguous group: sidx u32[], offs u64[], lens u32[], ooffs u64[], salts u64[]
+    struct Group {
+        int op;
+        uint32_t count;
+        size_t o_sidx, o_offs, o_lens, o_ooffs, o_salts;
+    };
+    std::vector<Group> groups;
+    std::vector<int64_t> group_of(size_t(rounds) * 2, -1);   // (sub-round, op) -> group
+    size_t m = 0;
+    for (uint32_t r = 0; r < rounds; r++)
+        for (int op = 0; op < 2; op++) {
+            uint32_t c = 0;
+            for (const Item &it : b->items)
+                c += it.round == r && it.op == op;
+            if (!c)
+                continue;
+            Group g{op, c, 0, 0, 0, 0, 0};
+            g.o_sidx = m;
+            m = up(m + 4 * size_t(c), 8);
+            g.o_offs = m;
+            m = up(m + 8 * size_t(c), 8);
+            g.o_lens = m;
+            m = up(m + 4 * size_t(c), 8);
+            g.o_ooffs = m;
+            m = up(m + 8 * size_t(c), 8);
+            g.o_salts = m;
+            m = up(m + 8 * size_t(c), 8);
+            if (m > b->meta_cap) {
+                set_err("metadata overflow");
+                return BRB_BATCH_NOT_DONE;
+            }
+            uint32_t k = 0;
+            for (const Item &it : b->items) {
+                if (it.round != r || it.op != op)
+                    continue;
+                reinterpret_cast<uint32_t *>(b->h_meta + g.o_sidx)[k] = uint32_t(op) * b->max_conns + it.conn;
+                reinterpret_cast<uint64_t *>(b->h_meta + g.o_offs)[k] = it.in_off;
+                reinterpret_cast<uint32_t *>(b->h_meta + g.o_lens)[k] = it.in_len;
+                reinterpret_cast<uint64_t *>(b->h_meta + g.o_ooffs)[k] = it.out_off;
+                reinterpret_cast<uint64_t *>(b->h_meta + g.o_salts)[k] = it.salt;
+                ++k;
+            }
+            group_of[size_t(r) * 2 + op] = int64_t(groups.size());
+            groups.push_back(g);
+        }
+    // valid flags: one byte per item of each read group, after the metadata
+    const size_t o_valid = m;
+    if (o_valid + n > b->meta_cap) {
+        set_err("metadata overflow");
+        return BRB_BATCH_NOT_DONE;
+    }
+    hipStream_t s = b->stream;
+    if ((e = hipMemcpyAsync(b->d_in, b->h_in, b->in_used, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(b->d_meta, b->h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return fail_hip("hipMemcpyAsync H2D", e);
+    size_t vpos = o_valid;
+    std::vector<size_t> group_valid(groups.size(), 0);
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        const Group &g = groups[gi];
+        const uint32_t *sidx = reinterpret_cast<const uint32_t *>(b->d_meta + g.o_sidx);
+        const uint64_t *offs = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_offs);
+        const uint32_t *lens = reinterpret_cast<const uint32_t *>(b->d_meta + g.o_lens);
+        const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_ooffs);
+        const uint64_t *salts = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_salts);
+        if (b->algo == BRB_CRYPTO_FUNC_RC4) {
+            // the output arena mirrors the input arena for RC4 (same offsets, same lengths)
+            e = brb::launch_rc4_crypt(b->d_states, b->d_in, b->d_out, offs, lens, g.count, s, sidx);
+        } else if (g.op == BRB_CRYPTO_OP_WRITE) {
+            e = brb::launch_rc4md5_frame(b->d_states, b->d_in, offs, lens, salts, b->d_out, ooffs, g.count, s, sidx);
+        } else {
+            // decrypt in place in the input arena, then the frames are copied out with it
+            group_valid[gi] = vpos;
+            e = brb::launch_rc4md5_open(b->d_states, b->d_in, b->d_in, offs, lens, g.count, b->d_meta + vpos, s, sidx);
+            vpos += g.count;
+        }
+        if (e != hipSuccess)
+            return fail_hip("kernel launch", e);
+    }
+    if ((e = hipMemcpyAsync(b->h_out, b->d_out, b->out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
+         (e = hipMemcpyAsync(b->h_in, b->d_in, b->in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+        (vpos > o_valid &&
+         (e = hipMemcpyAsync(b->h_meta + o_valid, b->d_meta + o_valid, vpos - o_valid, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return fail_hip("round completion", e);
+    // deliver in submission order; the k-th read item of a group has valid flag k of that group
+    std::vector<uint32_t> next_in_group(groups.size(), 0);
+    for (const Item &it : b->items) {
+        const int64_t gi = group_of[size_t(it.round) * 2 + it.op];
+        const uint32_t k = next_in_group[gi]++;
+        int valid = 1;
+        const uint8_t *out;
+        if (b->algo == BRB_CRYPTO_FUNC_RC4) {
+            out = b->h_out + it.in_off;
+        } else if (it.op == BRB_CRYPTO_OP_WRITE) {
+            out = b->h_out + it.out_off;
+        } else {
+            out = b->h_in + it.in_off;
+            valid = b->h_meta[group_valid[gi] + k];
+        }
+        if (done)
+            done(user, it.conn, it.op, out, it.out_len, valid);
+    }
+    b->items.clear();
+    b->in_used = b->out_used = 0;
+    return int64_t(n);
+}
+
+int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op, BRB_RC4_State *out)
+{
+    brb_api::clear_err();
+    if (!b || !out || conn >= b->max_conns || (op != BRB_CRYPTO_OP_READ && op != BRB_CRYPTO_OP_WRITE)) {
+        set_err("bad batcher, connection or op");
+        return BRB_BATCH_BADARG;
+    }
+    hipError_t e;
+    if ((e = hipMemcpyAsync(out, b->state(conn, op), sizeof(*out), hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(b->stream)) != hipSuccess)
+        return fail_hip("state copy", e);
+    return BRB_BATCH_OK;
+}
+
+}  // extern "C"

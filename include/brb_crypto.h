@@ -187,6 +187,39 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
                          const uint32_t *lengths, uint64_t n, uint8_t *valid, unsigned flags,
                          void *hip_stream);
 
+/* ---- Receive-loop batching ------------------------------------------------------
+ * The comm layer calls the transform hook once per buffer on the thread that owns the connection
+ * (EvAIOReqTransform_ReadData / _WriteData, ev_kq_aio_transform.c:42-70, from comm_tcp_server.c:1749,
+ * 1773, comm_tcp_client_read.c:176, 203, comm_tcp_server_conn.c:932).  A transform batcher takes the
+ * buffers of one event-loop round from many connections and runs them as one GPU call per
+ * direction.  It owns the read and write RC4 states of up to max_conns connections in HBM
+ * (CommEvCryptoInfo, libbrb_ev_comm.h:206-236).  Usage per round: Read/Write for every buffer,
+ * then Flush, which delivers every result through the callback in submission order.
+ * A connection's buffers stay in order: two buffers of one connection and direction in one round
+ * run as consecutive sub-rounds.
+ *   READ  (RC4_MD5): out = the decrypted frame, valid = EvAIOReqTransform_RC4_MD5_DataValidate;
+ *         the payload starts at out + BRB_RC4MD5_HEADER (the reference's MemBufferOffsetSet(30)).
+ *   WRITE (RC4_MD5): out = the 30 + len byte frame, salt = the caller's arc4random() value.
+ *   RC4: out = the RC4 stream of the buffer in either direction, valid = 1. */
+#define BRB_CRYPTO_FUNC_RC4       1       /* COMM_CRYPTO_FUNC_RC4, libbrb_ev_comm.h:166 */
+#define BRB_CRYPTO_FUNC_RC4_MD5   2       /* COMM_CRYPTO_FUNC_RC4_MD5, :167 */
+#define BRB_CRYPTO_OP_READ        0       /* CRYPTO_OPERATION_READ, libbrb_ev_aio.h:101 */
+#define BRB_CRYPTO_OP_WRITE       1       /* CRYPTO_OPERATION_WRITE, :102 */
+typedef struct BRB_TransformBatcher BRB_TransformBatcher;
+typedef void (*BRB_TransformDone)(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid);
+/* NULL on failure (reason in BRB_CryptoGPU_LastError).  A round holds at most max_round_bytes of
+ * input and 4 * max_conns buffers; Read/Write return 0 when it is full (Flush, then submit again). */
+BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t max_round_bytes, int algo);
+void BRB_TransformBatcherDestroy(BRB_TransformBatcher *b);
+/* EvAIOReqTransform_CryptoEnable (ev_kq_aio_transform.c:71-105): both states of `conn` = BRB_RC4_Init(key). */
+int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const void *key, int key_sz);
+int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
+int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
+/* Runs the round; returns the number of buffers delivered, or -1 / 0 as the batch calls do. */
+int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
+/* Copies a connection's current state (op = READ or WRITE) back to the host (tests, migration). */
+int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op, BRB_RC4_State *out);
+
 /* ---- base64 -----------------------------------------------------------------------
  * Encode = brb_base64_encode_to_mb (base64.c:304-361) for n records: record i = data[offsets[i] ..
  * + lengths[i]) -> out[out_offsets[i] .. + 4 * ceil(lengths[i] / 3)), standard alphabet, '='

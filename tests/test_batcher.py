@@ -1,0 +1,93 @@
+"""Receive-loop batching: a synthetic event loop drives BRB_TransformBatcher.
+
+Each round, a random subset of connections delivers 0..3 buffers (frames written by the peer with
+the oracle's RC4+MD5 write side) and sends 0..2 buffers.  The batcher's results must equal what the
+reference's per-buffer hook would produce for each connection in order (oracle), including the
+RC4 states after every round, frame validity and tampered frames.  The kqueue loop itself
+(ev_kq_base.c:589) is modelled, not run: libkqueue is not available here."""
+import numpy as np
+import pytest
+
+from brb_framework_amd import workload
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev(brb):
+    import torch
+    assert torch.cuda.is_available(), "no HIP device visible to torch"
+    assert brb.gpu_available(), brb.lib().BRB_CryptoGPU_LastError()
+    return torch
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_event_loop_rounds(brb, orc, torch_dev, algo):
+    rng = np.random.default_rng(algo)
+    C = 300
+    keys = [rng.integers(0, 256, int(rng.integers(4, 32)), dtype=np.uint8).tobytes() for _ in range(C)]
+    b = brb.TransformBatcher(C, 8 << 20, algo)
+    ours_r = [orc.rc4_init(k) for k in keys]      # oracle model of the batcher's read states
+    ours_w = [orc.rc4_init(k) for k in keys]      # ... and write states
+    peer_w = [orc.rc4_init(k) for k in keys]      # the peer's write side (produces what we read)
+    peer_r = [orc.rc4_init(k) for k in keys]      # the peer's read side (consumes what we write)
+    for c in range(C):
+        b.enable(c, keys[c])
+    for rnd in range(6):
+        expect = []
+        for c in rng.permutation(C)[: int(rng.integers(C // 3, C))]:
+            c = int(c)
+            for _ in range(int(rng.integers(0, 4))):      # received buffers, in order
+                n = int(rng.choice([0, 1, 5, 29, 64, 100, 1500, 4000]))
+                payload = workload.gen_records(0x5EED00F2 + rnd, c * 16 + len(expect), 1, n).tobytes() if n else b""
+                if algo == 2:
+                    peer_w[c], frame = orc.rc4md5_frame(peer_w[c], payload, rnd * 1000 + c)
+                    if rng.random() < 0.1 and len(frame) > 31:
+                        frame = bytearray(frame)
+                        frame[int(rng.integers(8, len(frame)))] ^= 4      # tampered on the wire
+                        frame = bytes(frame)
+                    ours_r[c], dec, ok = orc.rc4md5_open(ours_r[c], frame)
+                    expect.append((c, 0, dec, ok))
+                    assert b.read(c, frame) == 1
+                else:
+                    peer_w[c], wire = orc.rc4_crypt(peer_w[c], payload)
+                    ours_r[c], dec = orc.rc4_crypt(ours_r[c], wire)
+                    expect.append((c, 0, dec, 1))
+                    assert b.read(c, wire) == 1
+            for _ in range(int(rng.integers(0, 3))):      # outgoing buffers, in order
+                n = int(rng.choice([0, 3, 77, 1500]))
+                payload = workload.gen_records(0x5EED00F3 + rnd, c * 16 + len(expect), 1, n).tobytes() if n else b""
+                salt = int(rng.integers(0, 2**32))
+                if algo == 2:
+                    ours_w[c], frame = orc.rc4md5_frame(ours_w[c], payload, salt)
+                    peer_r[c], dec, ok = orc.rc4md5_open(peer_r[c], frame)
+                    assert ok == 1 and dec[30:] == payload
+                    expect.append((c, 1, frame, 1))
+                else:
+                    ours_w[c], wire = orc.rc4_crypt(ours_w[c], payload)
+                    expect.append((c, 1, wire, 1))
+                assert b.write(c, payload, salt) == 1
+        got = b.flush()
+        assert len(got) == len(expect)
+        for g, e in zip(got, expect):
+            assert g[0] == e[0] and g[1] == e[1] and g[2] == e[2] and g[3] == e[3], (rnd, e[0], e[1])
+        for c in range(0, C, 7):
+            assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
+    b.close()
+
+
+def test_round_full_and_bad_args(brb, torch_dev):
+    b = brb.TransformBatcher(2, 1000, 2)
+    with pytest.raises(RuntimeError):
+        b.enable(5, b"k")                         # connection id out of range
+    b.enable(0, b"key")
+    assert b.read(1, b"x") == -1                 # not enabled
+    assert b.read(0, bytes(600)) == 1
+    assert b.read(0, bytes(600)) == 0            # round full: flush first
+    assert len(b.flush()) == 1
+    assert b.read(0, bytes(600)) == 1
+    for _ in range(7):
+        b.write(0, b"", 0)
+    assert b.write(0, b"", 0) == 0               # 4 buffers per connection on average
+    assert len(b.flush()) == 8
+    b.close()
