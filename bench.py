@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5"],
+    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher"],
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B)")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the timed steps alternate over")
@@ -120,7 +120,9 @@ def main():
     cfg = workload.CONFIGS[cfg_id]
     stream = torch.cuda.current_stream(dev)
 
-    if args.op in ("rc4", "rc4md5"):
+    if args.op == "batcher":
+        result = bench_batcher(args, rank, world, log)
+    elif args.op in ("rc4", "rc4md5"):
         result = bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif cfg["op"] == "blowfish":
         result = bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
@@ -488,6 +490,38 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                                   "sample": f"oracle frame+open of {m} connections x {L} B, {reps} passes, {th} pthreads"}
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")
     return result
+
+
+# ------------------------------------------------------------------------------------------------
+def bench_batcher(args, rank, world, log):
+    """SURVEY §8 f2, host-inclusive: one event-loop round = C connections each receiving one
+    1500-byte RC4+MD5 frame and sending one 1500-byte payload, driven from C the way an event loop
+    would (tools/batcher_bench.c: one BRB_TransformBatcherRead/Write call per buffer, one Flush per
+    round).  Run as a child process (it opens the GPU itself)."""
+    exe = os.path.join(ROOT, "tools", "batcher_bench")
+    src = exe + ".c"
+    lib = os.path.join(ROOT, "brb_framework_amd")
+    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+        subprocess.run(["gcc", "-O2", "-I", os.path.join(ROOT, "include"), src, "-L", lib, "-lbrb_crypto_gpu",
+                        f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+    C = args.records_per_gpu or 16384
+    out = subprocess.run([exe, str(C), "1500", str(args.steps), str(args.warmup)], check=True, capture_output=True,
+                         text=True, timeout=600).stdout
+    r = json.loads(out.strip().splitlines()[-1])
+    if "error" in r:
+        raise SystemExit("batcher_bench: " + r["error"])
+    t = r["round_ms_median"] / 1e3
+    return {"metric": "GiB/s of payload through the receive-loop transform batcher (SURVEY §8 f2, host-inclusive)",
+            "value": r["payload_gib_s"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (peer frames built with the compat BRB_RC4/BRB_MD5 calls outside the timed region)",
+            "config": {"workload": f"f2: {C} connections x (1 frame in + 1 payload out) x 1500 B per round",
+                       "op": "tools/batcher_bench.c: BRB_TransformBatcherRead/Write per buffer + Flush per round",
+                       "parallelism": "single GPU"},
+            "buffers_per_s": r["buffers_per_s"], "round_ms_min": r["round_ms_min"],
+            "note": "step = one round: per-buffer submit (copy into the pinned arena), H2D, open + frame kernels, "
+                    "D2H, one callback per buffer"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,120 @@
+/*
+ * batcher_bench.c -- host-inclusive benchmark of the receive-loop transform batcher
+ * as a C event loop would drive it: per round, every connection receives one RC4+MD5 frame written
+ * by its peer and sends one payload; each buffer is one BRB_TransformBatcherRead/Write call, then
+ * one Flush delivers the results.  The peer side is built with the library's own compat surface
+ * (BRB_RC4_Crypt + BRB_MD5*), outside the timed region.  Prints one JSON object.
+ *
+ * Build: gcc -O2 -I include tools/batcher_bench.c -L brb_framework_amd -lbrb_crypto_gpu \
+ *            -Wl,-rpath,$PWD/brb_framework_amd -o tools/batcher_bench
+ * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3]
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "brb_crypto.h"
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+typedef struct {
+    unsigned long long delivered, valid, bytes;
+} Tally;
+
+static void on_done(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid)
+{
+    Tally *t = (Tally *)user;
+    (void)conn;
+    (void)op;
+    (void)out;
+    t->delivered++;
+    t->valid += valid != 0;
+    t->bytes += out_len;
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+    double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+int main(int argc, char **argv)
+{
+    const uint32_t C = argc > 1 ? (uint32_t)atoi(argv[1]) : 16384;
+    const uint32_t L = argc > 2 ? (uint32_t)atoi(argv[2]) : 1500;
+    const int R = argc > 3 ? atoi(argv[3]) : 20, W = argc > 4 ? atoi(argv[4]) : 3;
+    const uint32_t F = L + BRB_RC4MD5_HEADER;
+    unsigned char *payload = malloc((size_t)C * L), *frames = malloc((size_t)C * F);
+    BRB_RC4_State *peer = malloc(sizeof(BRB_RC4_State) * C);
+    unsigned char key[16];
+    unsigned long long x = 0x5EED00F2ull;
+    for (size_t i = 0; i < (size_t)C * L; i++) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        payload[i] = (unsigned char)(x >> 56);
+    }
+    BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) + 4096, BRB_CRYPTO_FUNC_RC4_MD5);
+    if (!b) {
+        printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
+        return 1;
+    }
+    for (uint32_t c = 0; c < C; c++) {
+        for (int k = 0; k < 16; k++)
+            key[k] = (unsigned char)(c * 131 + k * 7);
+        memset(&peer[c], 0, sizeof(peer[c]));
+        BRB_RC4_Init(&peer[c], key, 16);
+        if (BRB_TransformBatcherEnable(b, c, key, 16) != BRB_BATCH_OK) {
+            printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
+            return 1;
+        }
+    }
+    double *t = malloc(sizeof(double) * R);
+    Tally tally = {0, 0, 0};
+    for (int r = 0; r < W + R; r++) {
+        /* the peers' frames for this round (ev_kq_aio_transform.c:212-230 + :281-283) */
+        for (uint32_t c = 0; c < C; c++) {
+            unsigned char *f = frames + (size_t)c * F;
+            BRB_MD5_CTX m;
+            BRB_MD5Init(&m);
+            BRB_MD5Update(&m, payload + (size_t)c * L, L);
+            BRB_MD5Final(&m);
+            unsigned long salt = (unsigned long)(r * 1000003u + c);
+            memcpy(f, &salt, 8);
+            memcpy(f + 8, "HASH:", 5);
+            memcpy(f + 13, m.digest, 16);
+            f[29] = 0;
+            memcpy(f + 30, payload + (size_t)c * L, L);
+            BRB_RC4_Crypt(&peer[c], f, f, (int)F);
+        }
+        Tally round = {0, 0, 0};
+        const double t0 = now();
+        for (uint32_t c = 0; c < C; c++) {
+            BRB_TransformBatcherRead(b, c, frames + (size_t)c * F, F);
+            BRB_TransformBatcherWrite(b, c, payload + (size_t)c * L, L, c);
+        }
+        const int64_t n = BRB_TransformBatcherFlush(b, on_done, &round);
+        const double dt = now() - t0;
+        if (n != 2 * (int64_t)C || round.valid != round.delivered) {
+            printf("{\"error\": \"round %d: %lld delivered, %llu valid: %s\"}\n", r, (long long)n, round.valid,
+                   BRB_CryptoGPU_LastError());
+            return 1;
+        }
+        if (r >= W) {
+            t[r - W] = dt;
+            tally.delivered += round.delivered;
+            tally.valid += round.valid;
+        }
+    }
+    qsort(t, R, sizeof(double), cmp_d);
+    const double med = t[R / 2];
+    printf("{\"connections\": %u, \"bytes\": %u, \"rounds\": %d, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
+           "\"payload_gib_s\": %.3f, \"buffers_per_s\": %.0f, \"valid\": %llu, \"delivered\": %llu}\n",
+           C, L, R, med * 1e3, t[0] * 1e3, 2.0 * C * L / med / (1 << 30), 2.0 * C / med, tally.valid, tally.delivered);
+    BRB_TransformBatcherDestroy(b);
+    return 0;
+}
