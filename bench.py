@@ -39,8 +39,11 @@ L3_BYTES = 256 << 20
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps K (default: enough for >= 0.3 s of timed GPU work, at least 200)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warm-up steps W (default: as many as fill >= 1 s, so the GPU clock has "
+                         "ramped up before the timed region)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher"],
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B)")
@@ -135,6 +138,45 @@ def main():
 
 
 # ------------------------------------------------------------------------------------------------
+def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.3):
+    """W untimed steps, then the choice of K.  Explicit --warmup / --steps are used as given.  By
+    default the GPU is kept busy for >= warm_s before timing: a fresh MI355X starts at a low clock
+    and ramps over hundreds of ms (cfg2 MD5: 30.4 us per launch after 20 warm-up steps, 25.4 us at
+    steady state), and K fills >= timed_s of GPU time.  Step k goes to streams[k % len(streams)].
+    Returns (W, K); K is the same on every rank (max over ranks)."""
+    n = 0
+    step_s = None
+    if args.warmup is not None:
+        for k in range(args.warmup):
+            launch(k, streams[k % len(streams)], k % len(streams))
+        torch.cuda.synchronize()
+        n = args.warmup
+    else:
+        t0, chunk = time.perf_counter(), 4
+        while True:
+            tc = time.perf_counter()
+            for _ in range(chunk):
+                launch(n, streams[n % len(streams)], n % len(streams))
+                n += 1
+            torch.cuda.synchronize()
+            step_s = (time.perf_counter() - tc) / chunk
+            if time.perf_counter() - t0 >= warm_s:
+                break
+            chunk = min(chunk * 2, max(4, int(0.1 / max(step_s, 1e-7))))
+    if args.steps is not None:
+        k = args.steps
+    else:
+        if step_s is None:
+            tc = time.perf_counter()
+            for _ in range(8):
+                launch(n, streams[n % len(streams)], n % len(streams))
+                n += 1
+            torch.cuda.synchronize()
+            step_s = (time.perf_counter() - tc) / 8
+        k = max(200, math.ceil(timed_s / step_s))
+    return n, int(max_over_ranks(float(k)))
+
+
 def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     """K steps between barrier + synchronize on both sides; step k is enqueued on
     streams[k % len(streams)] straight through the C ABI (pre-resolved ctypes arguments, so the
@@ -206,16 +248,16 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         if rc != 1:
             raise RuntimeError(brb.lib().BRB_CryptoGPU_LastError().decode())
 
-    for k in range(args.warmup):                                # eager warm-up on every stream
-        launch(k, all_streams[k % len(all_streams)], k % len(all_streams))
-    torch.cuda.synchronize()
+    for j, s_ in enumerate(all_streams):                        # one eager call per stream
+        launch(j, s_, j)
+    n_warm, n_steps = warm_up(args, launch_raw, all_streams, torch, max_over_ranks)
     main_streams = [stream] if n_streams == 1 else side[:n_streams]
-    wall, ev_s = timed_steps(lambda k, s, j: launch_raw(k + args.warmup, s, j), args.steps, main_streams,
+    wall, ev_s = timed_steps(lambda k, s, j: launch_raw(k + n_warm, s, j), n_steps, main_streams,
                              barrier, max_over_ranks, torch)
     wall2 = None
     if args.two_stream:
         # the same K steps alternating over two HIP streams (two batches in flight)
-        wall2, _ = timed_steps(launch_raw, args.steps, side[:2], barrier, max_over_ranks, torch)
+        wall2, _ = timed_steps(launch_raw, n_steps, side[:2], barrier, max_over_ranks, torch)
     out = outs[0]
 
     # spot-check the last step's digests against hashlib (stdlib, independent of this repo)
@@ -224,12 +266,12 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     for i in list(np.random.default_rng(rank).integers(0, n_rank, 32)) + [0, n_rank - 1]:
         assert got[i].tobytes() == h(host[i * L:(i + 1) * L].tobytes()).digest(), f"digest mismatch at {i}"
 
-    total_bytes = n_global * L * args.steps
+    total_bytes = n_global * L * n_steps
     gib_s = total_bytes / wall / 2**30
-    mrec_s = n_global * args.steps / wall / 1e6
+    mrec_s = n_global * n_steps / wall / 1e6
     # per-launch duration from the events around the timed region (single stream: launches run back
     # to back, so this is the kernel time plus the ~2 us dependent-kernel boundary)
-    avg_kern_s = ev_s / args.steps
+    avg_kern_s = ev_s / n_steps
     achieved = n_rank * L / avg_kern_s / 1e9
     traffic = load_traffic(args.pmc_summary, f"cfg{cfg_id}_{args.op}")
     result = {
@@ -237,9 +279,9 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "value": round(gib_s, 2),
         "unit": "GiB/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "steps": n_steps,
+        "warmup": n_warm,
+        "ms_per_step": round(wall / n_steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -259,8 +301,8 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     }
     if wall2 is not None:
         result["two_stream_throughput"] = {
-            "value": round(n_global * L * args.steps / wall2 / 2**30, 2), "unit": "GiB/s",
-            "mrecords_per_s": round(n_global * args.steps / wall2 / 1e6, 3),
+            "value": round(n_global * L * n_steps / wall2 / 2**30, 2), "unit": "GiB/s",
+            "mrecords_per_s": round(n_global * n_steps / wall2 / 1e6, 3),
             "note": "same K steps alternating over 2 HIP streams (2 batches in flight)"}
     if world == 1 and not args.no_pcie:
         result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, dev, stream, log)
@@ -338,24 +380,22 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
         brb.blowfish_encrypt_batch(cdev, d, n_blocks, stream=s, async_=True)
         brb.blowfish_decrypt_batch(cdev, d, n_blocks, stream=s, async_=True)
 
-    for k in range(args.warmup):
-        launch(k, stream)
-    torch.cuda.synchronize()
-    wall, ev_s = timed_steps(launch, args.steps, [stream], barrier, max_over_ranks, torch)
+    n_warm, n_steps = warm_up(args, launch, [stream], torch, max_over_ranks)
+    wall, ev_s = timed_steps(launch, n_steps, [stream], barrier, max_over_ranks, torch)
     assert torch.equal(d, d0), "Blowfish round trip did not restore the plaintext"
     # one encrypt-only check against the oracle on a sample record
     brb.blowfish_encrypt_batch(cdev, d, n_blocks)
     wpr = cfg["rec_len"] // 8
     got = d[:wpr].cpu().numpy().view(np.uint64)
     assert np.array_equal(got, oracle.bf_ecb(oracle.bf_init(workload.CFG4_KEY), w[:wpr].copy()))
-    step_s = ev_s / args.steps
+    step_s = ev_s / n_steps
     plain = n_words * 8
     result = {
         "metric": "GiB/s of plaintext per Blowfish encrypt+decrypt round trip (cfg4)",
-        "value": round(plain * world * args.steps / wall / 2**30, 2),
+        "value": round(plain * world * n_steps / wall / 2**30, 2),
         "unit": "GiB/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "n_gpus": world, "steps": n_steps, "warmup": n_warm,
+        "ms_per_step": round(wall / n_steps * 1e3, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic (splitmix64 words, HBM-resident)",
         "config": {"workload": cfg["name"], "records_per_gpu": n_rec, "record_bytes": cfg["rec_len"],
@@ -435,26 +475,24 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         if rc != 1:
             raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
 
-    for k in range(args.warmup):
-        launch(k, stream)
-    torch.cuda.synchronize()
-    wall, ev_s = timed_steps(lambda k, s, j: launch(k + args.warmup, s, j), args.steps, [stream], barrier,
+    n_warm, n_steps = warm_up(args, launch, [stream], torch, max_over_ranks)
+    wall, ev_s = timed_steps(lambda k, s, j: launch(k + n_warm, s, j), n_steps, [stream], barrier,
                              max_over_ranks, torch)
     if args.op == "rc4md5":
         assert int(valid.sum()) == n, "a frame failed validation"
         assert torch.equal(wst, rst), "write and read states diverged"
         fr = frames[: 2 * (L + H)].cpu().numpy()
         assert fr[H:H + L].tobytes() == host[:L].tobytes()      # decrypted in place by the open step
-    step_s = ev_s / args.steps
+    step_s = ev_s / n_steps
     payload = n * L
     moved = 2 * payload if args.op == "rc4" else payload + 3 * n * (L + H)
     name = "BRB_RC4_CryptBatch" if args.op == "rc4" else "BRB_RC4MD5_FrameBatch + BRB_RC4MD5_OpenBatch"
     result = {
         "metric": f"GiB/s of payload per {'RC4 pass' if args.op == 'rc4' else 'RC4+MD5 frame + open round trip'} "
                   "(SURVEY §8 f1)",
-        "value": round(payload * world * args.steps / wall / 2**30, 2),
-        "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "value": round(payload * world * n_steps / wall / 2**30, 2),
+        "unit": "GiB/s", "n_gpus": world, "steps": n_steps, "warmup": n_warm,
+        "ms_per_step": round(wall / n_steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": f"synthetic (splitmix64 payloads, HBM-resident, {n_rot} rotating copies; random 16-byte keys)",
         "config": {"workload": f"f1: {n} connections x {L} B, 1 GPU" if world == 1 else f"f1: {n} connections/GPU",
@@ -505,15 +543,17 @@ def bench_batcher(args, rank, world, log):
         subprocess.run(["gcc", "-O2", "-I", os.path.join(ROOT, "include"), src, "-L", lib, "-lbrb_crypto_gpu",
                         f"-Wl,-rpath,{lib}", "-o", exe], check=True)
     C = args.records_per_gpu or 16384
-    out = subprocess.run([exe, str(C), "1500", str(args.steps), str(args.warmup)], check=True, capture_output=True,
+    steps = 20 if args.steps is None else args.steps
+    warm = 20 if args.warmup is None else args.warmup
+    out = subprocess.run([exe, str(C), "1500", str(steps), str(warm)], check=True, capture_output=True,
                          text=True, timeout=600).stdout
     r = json.loads(out.strip().splitlines()[-1])
     if "error" in r:
         raise SystemExit("batcher_bench: " + r["error"])
     t = r["round_ms_median"] / 1e3
     return {"metric": "GiB/s of payload through the receive-loop transform batcher (SURVEY §8 f2, host-inclusive)",
-            "value": r["payload_gib_s"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "value": r["payload_gib_s"], "unit": "GiB/s", "n_gpus": world, "steps": steps,
+            "warmup": warm, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (peer frames built with the compat BRB_RC4/BRB_MD5 calls outside the timed region)",
             "config": {"workload": f"f2: {C} connections x (1 frame in + 1 payload out) x 1500 B per round",

@@ -9,6 +9,7 @@
 // BrbSha1_Do (sha1.c:203-216) of data[r * rec_len .. (r + 1) * rec_len).
 #pragma once
 
+#include "digest_line.h"
 #include "dma_stage.h"
 
 namespace brb_digest {
@@ -161,6 +162,12 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
     constexpr int W = 4;
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs_needed = (groups + W - 1) / W;
+    // More than one wave per SIMD and 4-byte record bases with an odd dword stride (the record
+    // offsets within a line then take every dword position, so the window's ds_read_b32 are free of
+    // bank conflicts): line-aligned staging, digest_line.h.  1 Mi x 1500 B: 332 -> 305 us
+    // (tools/mb/md5_ab.hip).  At one wave per SIMD (cfg2) the two are even and this kernel stays.
+    if (groups > 1024 && line_supported(data, rec_len) && ((rec_len >> 2) & 1))
+        return launch_fixed_line<Alg>(data, rec_len, n_rec, out, out_al, s);
     if (rec_len > 64) {
         const unsigned g = unsigned(wgs_needed < 512 ? wgs_needed : 512);
         if (out_al)

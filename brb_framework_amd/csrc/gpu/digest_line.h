@@ -1,0 +1,213 @@
+// digest_line.h -- fixed-stride, lane-per-record digest kernel (MD5, SHA-1) with LINE-ALIGNED
+// LDS-DMA staging.  Used when every record starts on a 4-byte boundary (data 4-aligned and
+// rec_len % 4 == 0, e.g. the 1500-byte records of SURVEY §8(d) configs 2 and 5).
+//
+// Why line-aligned: a record of 1500 B starts anywhere inside a 128-byte memory line, so a
+// 128-byte stage taken at the record's own offset straddles two lines and every line is requested
+// twice.  Measured on the staging alone (tools/mb/dma_pattern.hip, 1 Mi x 1500 B): 5.8 TB/s with
+// record-relative 128-byte pieces, 6.5 TB/s with line-aligned ones (a contiguous stream: 6.3).
+//
+// Stage k of lane l's record = the k-th 128-byte line from the line holding the record's first
+// byte.  The record starts sh = (address mod 128) / 4 dwords into its first line, so message blocks
+// 2k-2 and 2k-1 (stream dwords sh + 32(k-1) .. sh + 32k - 1) lie in lines k-1 and k.  Lines k-1
+// and k sit in the two slots of the wave's LDS ring; each lane reads its 32 shifted dwords with
+// ds_read_b32 at per-lane addresses that are fixed for the whole record (one address table per
+// slot parity), so the shift costs no VALU.  Once the window is in VGPRs, the slot of line k-1 is
+// refilled with line k+1 while blocks 2k-2 and 2k-1 are hashed.
+//
+// Safety: every line read holds at least one byte of the batch (the line of a record's first byte,
+// the lines after it up to the line of the batch's last byte); lines past that are cut off by the
+// buffer descriptor's range check and read as zeros.  Bytes of a line outside the record are
+// masked by the padding step, as the tail of any record.
+//
+// Record r's digest = BRB_MD5Init/Update/Final (md5.c:38-168) or BrbSha1_Do (sha1.c:203-216) of
+// data[r * rec_len .. (r + 1) * rec_len).
+#pragma once
+
+#include "dma_stage.h"
+
+namespace brb_digest {
+
+// Padding, digest and store of one group: the record's tail block (if any) is window half
+// nfull - (2K - 2) of the last iteration; bytes past the record are masked (md5.c:134-168).
+template <class Alg, bool OUT_ALIGNED>
+BRB_DEV void line_finish(typename Alg::State &st, const uint32_t (&w0)[16], const uint32_t (&w1)[16], uint32_t t,
+                         uint32_t nfull, uint32_t K, uint32_t rec_len, uint8_t *out, uint64_t r, uint64_t n_rec)
+{
+    uint32_t w[16];
+    uint32_t tt = t;
+    asm volatile("" : "+s"(tt));                               // keep the tail math here, once per group
+    if (tt && nfull + 2 - 2 * K) {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            w[i] = w1[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            w[i] = tt ? w0[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+        const uint32_t o = 4 * i;
+        const uint32_t keep = tt > o ? (tt - o < 4 ? tt - o : 4) : 0;
+        uint32_t v = w[i] & uint32_t((uint64_t(1) << (8 * keep)) - 1);
+        if (tt >= o && tt < o + 4)
+            v |= 0x80u << (8 * (tt - o));
+        w[i] = v;
+    }
+    Alg::finish(st, w, t, rec_len);
+    if (r < n_rec)
+        Alg::template store<OUT_ALIGNED>(out, r, st);
+}
+
+// launch_bounds min 2 waves per SIMD: two 4-wave workgroups per CU (64 KiB of LDS each).
+template <class Alg, int WAVES, bool OUT_ALIGNED>
+__global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
+                                                                     uint64_t n_rec, uint8_t *__restrict__ out)
+{
+    constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
+    const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
+    if (wave0 >= n_groups)
+        return;
+
+    const uint32_t my_off = wv * 2 * SLOT;                     // slot 0; slot 1 = my_off + SLOT (bit 13 clear)
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + my_off;
+    const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
+    const uint32_t nblk = nfull + (t ? 1 : 0);
+    const uint32_t K = (nblk + 1) >> 1;                        // 2-block iterations per group; K + 1 lines
+    const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    const uint64_t end_line = (dbase + n_rec * rec_len + 127) & ~uint64_t(127);
+    // 16-byte granule swizzle of a 128-byte row (applied on the DMA source): ds_read_b128 of one
+    // logical granule by all lanes is conflict-free, ds_read_b32 of one logical dword 4-way at worst.
+    auto swz = [](uint32_t row) { return (row >> 1) & 7; };
+
+    // ---- issue side: DMA lane j of instruction q stages granule j % 8 of row 8q + j / 8
+    uint32_t vq[8];
+    uint64_t gline = 0;                                        // first line of the issuing group
+    auto dma_setup = [&](uint64_t g) {
+        const uint64_t r0 = g * 64;
+        const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
+        const uint64_t a0 = dbase + r0 * rec_len;
+        gline = a0 & ~uint64_t(127);
+        const uint32_t o0 = uint32_t(a0) & 127;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t row = 8 * q + (lane >> 3);
+            const uint32_t rr = row < last ? row : last;
+            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row));
+        }
+    };
+    auto issue = [&](uint32_t slot, uint32_t k) {              // line k of the issuing group -> slot
+        const uint64_t base = gline + 128ull * k;
+        const brb_dma::v4i rs =
+            brb_dma::make_rsrc(reinterpret_cast<const uint8_t *>(base), end_line > base ? end_line - base : 0);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\t"
+                "s_mov_b32 m0, %3\n\t"
+                "s_nop 0\n\t"
+                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(vq[q]), "s"(rs), "s"(lds0 + slot * SLOT + 1024u * q)
+                : "memory");
+        }
+    };
+
+    // ---- read side: window dword i of this lane -> LDS offset, for lines (k-1, k) in slots
+    // (0, 1) ["ae", k odd] and (1, 0) ["ao", k even]
+    uint32_t ae[32], ao[32];
+    auto win_setup = [&](uint64_t g) {
+        const uint64_t r0 = g * 64;
+        const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
+        const uint32_t o0 = uint32_t(dbase + r0 * rec_len) & 127;
+        const uint32_t rr = lane < last ? lane : last;
+        const uint32_t sh = ((o0 + rr * rec_len) & 127) >> 2;
+        const uint32_t f = swz(lane), row = my_off + lane * 128;
+#pragma unroll
+        for (uint32_t i = 0; i < 32; i++) {
+            const uint32_t q = sh + i, qq = q & 31;
+            const uint32_t a = row + ((((qq >> 2) ^ f) << 4) | ((qq & 3) << 2));
+            ae[i] = q >= 32 ? a + SLOT : a;
+            ao[i] = q >= 32 ? a : a + SLOT;
+        }
+    };
+
+    uint32_t w0[16], w1[16];
+    auto read_window = [&](const uint32_t (&ad)[32]) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            w0[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
+            w1[i] = *reinterpret_cast<const uint32_t *>(ring + ad[16 + i]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // window in VGPRs before its slot is refilled
+    };
+
+    uint64_t g = wave0;
+    dma_setup(g);
+    issue(0, 0);
+    issue(1, 1);
+    win_setup(g);
+    for (;;) {
+        typename Alg::State st = Alg::iv();
+        // one iteration: wait for line k, read the window, refill the slot of line k-1 (or start
+        // the next group), hash blocks 2k-2 and 2k-1
+        // one compress site per block (the code must stay small: one wave per SIMD runs out of
+        // the shared instruction cache at once when the loop body is unrolled)
+        for (uint32_t k = 1; k <= K; k++) {
+            brb_dma::wait_vmcnt<0>();
+            if (k & 1)
+                read_window(ae);
+            else
+                read_window(ao);
+            if (k < K) {
+                issue((k + 1) & 1, k + 1);
+            } else if (g + wstride < n_groups) {
+                dma_setup(g + wstride);
+                issue(0, 0);
+                issue(1, 1);
+            }
+            const uint32_t b = 2 * k - 2;
+            if (b < nfull)
+                Alg::compress(st, w0);
+            if (b + 1 < nfull)
+                Alg::compress(st, w1);
+        }
+        line_finish<Alg, OUT_ALIGNED>(st, w0, w1, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
+        g += wstride;
+        if (g >= n_groups)
+            break;
+        win_setup(g);
+    }
+}
+
+// Line-aligned staging needs 4-byte record bases (the window shift is whole dwords).
+inline bool line_supported(const uint8_t *data, uint32_t rec_len)
+{
+    return rec_len > 64 && (rec_len & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0 &&
+           uint64_t(rec_len) * 64 + 256 < (uint64_t(1) << 31);
+}
+
+template <class Alg>
+hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
+                             hipStream_t s)
+{
+    constexpr int W = 4;
+    const uint64_t groups = (n_rec + 63) / 64;
+    const uint64_t wgs_needed = (groups + W - 1) / W;
+    const unsigned g = unsigned(wgs_needed < 512 ? wgs_needed : 512);   // 2 workgroups per CU, persistent
+    if (out_al)
+        digest_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    else
+        digest_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    return hipGetLastError();
+}
+
+}  // namespace brb_digest

@@ -23,6 +23,18 @@ BRB_DEV Md5State md5_iv()
     return Md5State{0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
 }
 
+// Round-3 step (F3 = b ^ c ^ d) with v_xad_u32 = (b ^ cd) + x: cd = c ^ d and x = a + m + K do not
+// depend on b, so the step's dependent chain is xad -> alignbit -> add (3 ops, 5 VALU per step)
+// instead of xor -> add3 -> alignbit -> add (hipcc's lowering of the plain macro, 6 VALU).
+#define BRB_MD5_STEP3X(a, b, c, d, m, k, s)                                               \
+    do {                                                                                 \
+        const uint32_t x_ = (a) + (m) + (k), cd_ = (c) ^ (d);                            \
+        uint32_t f_;                                                                     \
+        asm("v_xad_u32 %0, %1, %2, %3" : "=v"(f_) : "v"(b), "v"(cd_), "v"(x_));          \
+        (a) = (b) + rotl<s>(f_);                                                         \
+    } while (0)
+
+template <bool XAD = true>
 BRB_DEV void md5_compress(Md5State &st, const uint32_t (&m)[16])
 {
     uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
@@ -61,22 +73,22 @@ BRB_DEV void md5_compress(Md5State &st, const uint32_t (&m)[16])
     BRB_MD5_STEP(BRB_MD5_F2, c, d, a, b, m[7], 0x676f02d9u, 14);
     BRB_MD5_STEP(BRB_MD5_F2, b, c, d, a, m[12], 0x8d2a4c8au, 20);
 
-    BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[5], 0xfffa3942u, 4);
-    BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[8], 0x8771f681u, 11);
-    BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[11], 0x6d9d6122u, 16);
-    BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[14], 0xfde5380cu, 23);
-    BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[1], 0xa4beea44u, 4);
-    BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-    BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-    BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[10], 0xbebfbc70u, 23);
-    BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[13], 0x289b7ec6u, 4);
-    BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[0], 0xeaa127fau, 11);
-    BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[3], 0xd4ef3085u, 16);
-    BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[6], 0x04881d05u, 23);
-    BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[9], 0xd9d4d039u, 4);
-    BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[12], 0xe6db99e5u, 11);
-    BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-    BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[2], 0xc4ac5665u, 23);
+    if constexpr (XAD) BRB_MD5_STEP3X(a, b, c, d, m[5], 0xfffa3942u, 4); else BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[5], 0xfffa3942u, 4);
+    if constexpr (XAD) BRB_MD5_STEP3X(d, a, b, c, m[8], 0x8771f681u, 11); else BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[8], 0x8771f681u, 11);
+    if constexpr (XAD) BRB_MD5_STEP3X(c, d, a, b, m[11], 0x6d9d6122u, 16); else BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    if constexpr (XAD) BRB_MD5_STEP3X(b, c, d, a, m[14], 0xfde5380cu, 23); else BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[14], 0xfde5380cu, 23);
+    if constexpr (XAD) BRB_MD5_STEP3X(a, b, c, d, m[1], 0xa4beea44u, 4); else BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[1], 0xa4beea44u, 4);
+    if constexpr (XAD) BRB_MD5_STEP3X(d, a, b, c, m[4], 0x4bdecfa9u, 11); else BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    if constexpr (XAD) BRB_MD5_STEP3X(c, d, a, b, m[7], 0xf6bb4b60u, 16); else BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    if constexpr (XAD) BRB_MD5_STEP3X(b, c, d, a, m[10], 0xbebfbc70u, 23); else BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    if constexpr (XAD) BRB_MD5_STEP3X(a, b, c, d, m[13], 0x289b7ec6u, 4); else BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    if constexpr (XAD) BRB_MD5_STEP3X(d, a, b, c, m[0], 0xeaa127fau, 11); else BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[0], 0xeaa127fau, 11);
+    if constexpr (XAD) BRB_MD5_STEP3X(c, d, a, b, m[3], 0xd4ef3085u, 16); else BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    if constexpr (XAD) BRB_MD5_STEP3X(b, c, d, a, m[6], 0x04881d05u, 23); else BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[6], 0x04881d05u, 23);
+    if constexpr (XAD) BRB_MD5_STEP3X(a, b, c, d, m[9], 0xd9d4d039u, 4); else BRB_MD5_STEP(BRB_MD5_F3, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    if constexpr (XAD) BRB_MD5_STEP3X(d, a, b, c, m[12], 0xe6db99e5u, 11); else BRB_MD5_STEP(BRB_MD5_F3, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    if constexpr (XAD) BRB_MD5_STEP3X(c, d, a, b, m[15], 0x1fa27cf8u, 16); else BRB_MD5_STEP(BRB_MD5_F3, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    if constexpr (XAD) BRB_MD5_STEP3X(b, c, d, a, m[2], 0xc4ac5665u, 23); else BRB_MD5_STEP(BRB_MD5_F3, b, c, d, a, m[2], 0xc4ac5665u, 23);
 
     BRB_MD5_STEP(BRB_MD5_F4, a, b, c, d, m[0], 0xf4292244u, 6);
     BRB_MD5_STEP(BRB_MD5_F4, d, a, b, c, m[7], 0x432aff97u, 10);

@@ -118,6 +118,25 @@ def test_cfg3_full(brb, orc, torch_dev, golden):
         assert got5[e["r"]].tobytes().hex() == e["md5"]
 
 
+@pytest.mark.parametrize("n,rec_len,off", [
+    (65600, 1500, 0),        # > 1024 groups of 64: line-aligned staging (digest_line.h)
+    (65600, 1500, 4),        # record bases 4 mod 16: every per-lane window shift changes
+    (65601, 1532, 8),        # t = 60: two padding blocks; partial last group
+    (66000, 1508, 12),       # t = 36
+    (65700, 132, 4),         # 3 lines per record, K = 2
+    (65600, 1504, 0),        # even dword stride: record-relative staging (digest_dma.h)
+])
+def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
+    data = workload.gen_records(0x5EED0006, 0, n, rec_len)
+    d = torch_dev.zeros(data.size + 64, dtype=torch_dev.uint8, device="cuda")
+    d[off:off + data.size] = to_dev(torch_dev, data)
+    view = d[off:off + data.size]
+    assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.md5_batch_fixed(data, rec_len, n, threads=16))
+    assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+
+
 def test_cfg5_shard_property(brb, torch_dev):
     """One GPU's shard of cfg5 (records [7/8 N, N)): sampled records vs hashlib."""
     n_all, L = workload.CONFIGS[5]["records"], workload.CONFIGS[5]["rec_len"]

@@ -13,8 +13,8 @@ run cfg2_md5 --no-pcie --no-cpu-baseline &&
 run cfg2_md5_2s --two-stream --no-pcie --no-cpu-baseline &&
 run cfg2_sha1 --op sha1 --no-pcie --no-cpu-baseline &&
 run cfg3_md5 --config 3 --no-pcie --no-cpu-baseline &&
-run cfg5_md5 --config 5 --steps 50 --warmup 5 --no-pcie --no-cpu-baseline &&
-run cfg4_bf --config 4 --steps 50 --warmup 10 &&
-run f1_rc4 --op rc4 --steps 50 --warmup 5 --no-cpu-baseline &&
-run f1_rc4md5 --op rc4md5 --steps 50 --warmup 5 &&
-run f2_batcher --op batcher --steps 20 --warmup 3
+run cfg5_md5 --config 5 --no-pcie --no-cpu-baseline &&
+run cfg4_bf --config 4 &&
+run f1_rc4 --op rc4 --no-cpu-baseline &&
+run f1_rc4md5 --op rc4md5 &&
+run f2_batcher --op batcher

@@ -13,7 +13,7 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-template <int BPS, int P, int WAVES>
+template <int BPS, int P, int WAVES, bool LINE_ALIGNED = false>
 __global__ __launch_bounds__(64 * WAVES) void stage_kernel(const uint8_t *data, uint32_t L, uint64_t n_rec, uint32_t *out)
 {
     constexpr int S = 64 * BPS, SLOT = 64 * S, NI = 4 * BPS, RPI = 1024 / S;   // records per instruction
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(64 * WAVES) void stage_kernel(const uint8_t *data, 
     for (int q = 0; q < NI; q++) {
         const uint32_t rec = q * RPI + rec_in;
         const uint32_t f = G == 4 ? (rec >> 2) & 3 : G == 8 ? (rec >> 1) & 7 : rec & 15;
-        vo[q] = rec * L + ((gran ^ f) % G) * 16;
+        vo[q] = (LINE_ALIGNED ? (rec * L) & ~127u : rec * L) + ((gran ^ f) % G) * 16;
     }
     const uint32_t nstage = (L / 64) / BPS;
     const uint32_t my_groups = uint32_t((n_groups - wave0 + wstride - 1) / wstride), total = my_groups * nstage;
@@ -123,6 +123,8 @@ int main(int argc, char **argv)
         {"S=64  P4", stage_kernel<1, 4, 4>, 4, 4 * 4 * 4096},
         {"S=128 P2", stage_kernel<2, 2, 4>, 4, 4 * 2 * 8192},
         {"S=128 P3", stage_kernel<2, 3, 4>, 4, 4 * 3 * 8192},
+        {"S=128 P2 line-aligned", stage_kernel<2, 2, 4, true>, 4, 4 * 2 * 8192},
+        {"S=128 P3 line-aligned", stage_kernel<2, 3, 4, true>, 4, 4 * 3 * 8192},
         {"S=256 P2", stage_kernel<4, 2, 4>, 4, 4 * 2 * 16384},
         {"linear 4KiB P3", linear_kernel<3, 4>, 4, 4 * 3 * 4096},
         {"linear 4KiB P4", linear_kernel<4, 4>, 4, 4 * 4 * 4096},

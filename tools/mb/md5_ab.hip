@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "digest_dma.h"
+#include "digest_line.h"
 #include "md5_device.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -65,6 +66,9 @@ struct AlgLit {      // product compress (m + K as a literal VOP2 add)
     template <bool A> static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st)
     { reinterpret_cast<uint4 *>(out)[r] = make_uint4(st.a, st.b, st.c, st.d); }
 };
+struct AlgOld : AlgLit {   // round 3 lowered by hipcc (xor, xor, add3)
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress<false>(st, w); }
+};
 struct AlgSK : AlgLit {
     static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress_sk(st, w); }
 };
@@ -101,18 +105,21 @@ int main(int argc, char **argv)
     uint8_t *o;
     CK(hipMalloc(&o, n * 16));
     struct V { const char *name; Kern k; int waves; int cap; };
-    std::vector<V> vs = {
-        {"BPS2 P3 (product)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 2, true>, 4, 256},
-        {"BPS2 P2", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 2, true>, 4, 512},
-        {"BPS1 P3", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 1, true>, 4, 768},
-        {"BPS1 P4", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 4, 1, true>, 4, 512},
-        {"BPS1 P2 (5 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 1, true>, 4, 1280},
-        {"BPS1 P2 (2 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 2, 1, true>, 4, 512},
-        {"BPS1 P3 (3 WG/CU)", brb_digest::digest_fixed_dma_kernel<AlgSK, 4, 3, 1, true>, 4, 768},
-        {"BPS2 P3 sched", brb_digest::digest_fixed_dma_kernel<AlgSched, 4, 3, 2, true>, 4, 256},
-        {"DMA only BPS2 P3", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, 2, true>, 4, 256},
-        {"DMA only BPS2 P2", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 2, true>, 4, 512},
-        {"DMA only BPS1 P3", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 3, 1, true>, 4, 768},
+    using namespace brb_digest;
+    std::vector<V> vs;
+    if (L > 64) vs = {
+        {"BPS2 P2 xad (product)", digest_fixed_dma_kernel<AlgLit, 4, 2, 2, true>, 4, 512},
+        {"LINE (line-aligned) P2", digest_line_kernel<AlgLit, 4, true>, 4, 512},
+        {"DMA only LINE", digest_line_kernel<AlgNull, 4, true>, 4, 512},
+        {"BPS2 P3 xad 1WG/CU", digest_fixed_dma_kernel<AlgLit, 4, 3, 2, true>, 4, 256},
+        {"DMA only BPS2 P2", digest_fixed_dma_kernel<AlgNull, 4, 2, 2, true>, 4, 512},
+    };
+    else vs = {
+        {"BPS1 P3 (product)", digest_fixed_dma_kernel<AlgLit, 4, 3, 1, true>, 4, 768},
+        {"BPS1 P3 old F3", digest_fixed_dma_kernel<AlgOld, 4, 3, 1, true>, 4, 768},
+        {"BPS1 P2 4WG/CU", digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4, 1024},
+        {"BPS1 P3 4WG/CU (3 fit)", digest_fixed_dma_kernel<AlgLit, 4, 3, 1, true>, 4, 1024},
+        {"DMA only BPS1 P3", digest_fixed_dma_kernel<AlgNull, 4, 3, 1, true>, 4, 768},
     };
     std::vector<uint8_t> ref(n * 16), got(n * 16);
     hipEvent_t e0, e1;
