@@ -1,6 +1,7 @@
 // digest_dma.h -- the fixed-stride, LDS-DMA staged, lane-per-record digest kernel shared by MD5
 // and SHA-1.  `Alg` supplies State, iv(), compress(st, w) on little-endian message words,
-// finish(st, w, t, len) on the padded tail block, and store<ALIGNED>(out, r, st).
+// finish(st, w, t, len) on the padded tail block, pad_only(st, len) for the constant padding block
+// of a record whose length is a multiple of 64, and store<ALIGNED>(out, r, st).
 //
 // Persistent waves: wave w digests record groups w, w + W_total, w + 2 W_total, ... (64 records
 // per group, one per lane).  A wave's work is one flat sequence of "stages" (group, block); the
@@ -103,6 +104,10 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         // (the hoisted form spilled ~200 SGPRs to VGPR lanes).
         uint32_t tt = t;
         asm volatile("" : "+s"(tt));
+        const uint64_t r = rb + lane;
+        if (tt == 0) {                                        // the padding block is a constant
+            Alg::pad_only(st, rec_len);
+        } else {
         if (tt) {
             sg.read(sp, nfull - b0, w);                       // the tail block of this stage
         } else {
@@ -112,7 +117,6 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         }
         // records ending within 3 bytes of the batch end: a staged dword of their tail may
         // straddle the end of the batch and was range-checked to zero -> re-read byte by byte
-        const uint64_t r = rb + lane;
         if (tt && r < n_rec && (n_rec - 1 - r) * rec_len < 4) {
             const uint8_t *a = data + r * rec_len + 64u * nfull;
 #pragma unroll
@@ -136,6 +140,7 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
             w[i] = v;
         }
         Alg::finish(st, w, t, rec_len);
+        }
         if (r < n_rec)
             Alg::template store<OUT_ALIGNED>(out, r, st);
         st = Alg::iv();
@@ -157,7 +162,7 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
     // Shapes measured with tools/mb/md5_ab.hip (interleaved, one process):
     //  * records > 64 B: 128-byte stages, ring of 2 (16 KiB per wave, 64 KiB per 4-wave workgroup,
     //    2 workgroups per CU): 1 Mi x 1500 B 335 us vs 388 us with 64-byte stages;
-    //  * records <= 64 B (one block + padding): 64-byte stages, ring of 3, 3 workgroups per CU.
+    //  * records <= 64 B (one block + padding): 64-byte stages, ring of 2, 4 workgroups per CU.
     // Persistent beyond the resident grid (waves loop over groups of 64 records).
     constexpr int W = 4;
     const uint64_t groups = (n_rec + 63) / 64;
@@ -175,11 +180,13 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
         else
             digest_fixed_dma_kernel<Alg, W, 2, 2, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
     } else {
-        const unsigned g = unsigned(wgs_needed < 768 ? wgs_needed : 768);
+        // 4 workgroups per CU (32 KiB each): 1 Mi x 64 B = 16 384 groups = exactly 4 per wave, no
+        // tail imbalance; 23.2 us vs 23.7 us for a ring of 3 at 3 workgroups per CU (warm, md5_ab)
+        const unsigned g = unsigned(wgs_needed < 1024 ? wgs_needed : 1024);
         if (out_al)
-            digest_fixed_dma_kernel<Alg, W, 3, 1, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+            digest_fixed_dma_kernel<Alg, W, 2, 1, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
         else
-            digest_fixed_dma_kernel<Alg, W, 3, 1, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+            digest_fixed_dma_kernel<Alg, W, 2, 1, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
     }
     return hipGetLastError();
 }

@@ -34,17 +34,23 @@ template <class Alg, bool OUT_ALIGNED>
 BRB_DEV void line_finish(typename Alg::State &st, const uint32_t (&w0)[16], const uint32_t (&w1)[16], uint32_t t,
                          uint32_t nfull, uint32_t K, uint32_t rec_len, uint8_t *out, uint64_t r, uint64_t n_rec)
 {
-    uint32_t w[16];
     uint32_t tt = t;
     asm volatile("" : "+s"(tt));                               // keep the tail math here, once per group
-    if (tt && nfull + 2 - 2 * K) {
+    if (tt == 0) {
+        Alg::pad_only(st, rec_len);                            // the padding block is a constant
+        if (r < n_rec)
+            Alg::template store<OUT_ALIGNED>(out, r, st);
+        return;
+    }
+    uint32_t w[16];
+    if (nfull + 2 - 2 * K) {
 #pragma unroll
         for (int i = 0; i < 16; i++)
             w[i] = w1[i];
     } else {
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            w[i] = tt ? w0[i] : 0u;
+            w[i] = w0[i];
     }
 #pragma unroll
     for (uint32_t i = 0; i < 16; i++) {

@@ -281,3 +281,14 @@ BRB_DEV void md5_finish(Md5State &st, uint32_t (&w)[16], uint32_t t, uint64_t to
     w[15] = uint32_t(total_len >> 29);
     md5_compress(st, w);
 }
+
+// The padding block of a message whose length is a multiple of 64 (md5.c:134-168 with t = 0):
+// 0x80, zeros, the bit length.  Compile-time words except the length (wave-uniform), so m + K folds
+// into constants and each step is 4 VALU instead of 5.
+BRB_DEV void md5_pad_only(Md5State &st, uint64_t total_len)
+{
+    uint32_t w[16] = {0x80u};
+    w[14] = uint32_t(total_len << 3);
+    w[15] = uint32_t(total_len >> 29);
+    md5_compress(st, w);
+}

@@ -30,6 +30,7 @@ struct Md5Alg {
     static BRB_DEV State iv() { return md5_iv(); }
     static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress(st, w); }
     static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { md5_finish(st, w, t, len); }
+    static BRB_DEV void pad_only(State &st, uint64_t len) { md5_pad_only(st, len); }
     template <bool ALIGNED>
     static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st) { Out16::store<ALIGNED>(out, r, st); }
 };

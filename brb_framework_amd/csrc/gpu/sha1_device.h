@@ -81,3 +81,13 @@ BRB_DEV void sha1_finish(Sha1State &st, uint32_t (&w)[16], uint32_t t, uint64_t 
     w[15] = uint32_t(len << 3);
     sha1_compress(st, w);
 }
+
+// The padding block of a message whose length is a multiple of 64 (t = 0 in sha1_finish): the
+// block and its whole schedule are constants except the two wave-uniform length words.
+BRB_DEV void sha1_pad_only(Sha1State &st, uint64_t len)
+{
+    uint32_t w[16] = {0x80000000u};
+    w[14] = uint32_t(len >> 29) + (len >= (uint64_t(1) << 29) ? 1u : 0u);
+    w[15] = uint32_t(len << 3);
+    sha1_compress(st, w);
+}

@@ -35,6 +35,7 @@ struct Sha1Alg {
         sha1_compress(st, w);
     }
     static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { sha1_finish(st, w, t, len); }
+    static BRB_DEV void pad_only(State &st, uint64_t len) { sha1_pad_only(st, len); }
     template <bool ALIGNED>
     static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st) { store20<ALIGNED>(out, r, st); }
 };

@@ -30,14 +30,47 @@ def pmc_means(d, pat):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def timed_region(trace_csv, pat, bench_json):
+    """Mean duration of the last K dispatches matching `pat` (K = the bench's timed steps; the
+    dispatches before them are the warm-up), next to the bench's own HIP-event launch average."""
+    try:
+        b = json.load(open(bench_json))
+    except (OSError, ValueError):
+        return None
+    per_step = 2 if "bf_rep" in pat else 1                     # cfg4: encrypt + decrypt per step
+    k = int(b["steps"]) * per_step
+    durs = []
+    for row in csv.DictReader(open(trace_csv)):
+        if pat in row["Kernel_Name"]:
+            durs.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    durs.sort()
+    last = [d for _, d in durs[-k:]]
+    if not last:
+        return None
+    r = b.get("roofline", {})
+    return {"kernel_filter": pat, "dispatches_total": len(durs), "timed_dispatches": len(last),
+            "rocprof_mean_us_timed_region": round(sum(last) / len(last) / 1e3, 3),
+            "rocprof_mean_us_all": round(sum(d for _, d in durs) / len(durs) / 1e3, 3),
+            "bench_event_us_per_step": r.get("launch_us_avg", r.get("step_us_avg")),
+            "note": "bench_event_us_per_step includes the dependent-launch gap between back-to-back kernels"}
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    for sub, name in (("prof", "bench_cfg2_md5"), ("prof4", "bench_cfg4_blowfish")):
+    for sub, name, pat, bj in (("prof", "bench_cfg2_md5", "Md5Alg", "bench_prof.json"),
+                               ("prof4", "bench_cfg4_blowfish", "bf_rep", "bench4_prof.json")):
         f = os.path.join(src, sub, "run_kernel_stats.csv")
         if os.path.exists(f):
             shutil.copy(f, os.path.join(prof, f"{tag}_{name}_kernel_stats.csv"))
+        t = os.path.join(src, sub, "run_kernel_trace.csv")
+        if os.path.exists(t):
+            tr = timed_region(t, pat, os.path.join(src, bj))
+            if tr:
+                with open(os.path.join(prof, f"{tag}_{name}_timed_region.json"), "w") as fo:
+                    json.dump(tr, fo, indent=1)
+                    fo.write("\n")
     traffic = {}
     for sub, key, pat in (("pmc2", "cfg2_md5", "Md5Alg"), ("pmc2s", "cfg2_sha1", "Sha1Alg"), ("pmc4", "cfg4_blowfish", "bf_rep_kernel")):
         d = os.path.join(src, sub)

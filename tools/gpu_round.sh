@@ -12,7 +12,7 @@ timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && ech
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline --no-pcie > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" && echo "rocprof ok" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- \
-    python3 bench.py --config 4 --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench4_prof.json" 2> "$OUT/bench4_prof.err" && echo "rocprof4 ok" &&
+    python3 bench.py --config 4 --no-cpu-baseline > "$OUT/bench4_prof.json" 2> "$OUT/bench4_prof.err" && echo "rocprof4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc2" --config 2 > /dev/null && echo "pmc2 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc2s" --config 2 --op sha1 > /dev/null && echo "pmc2s ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc4" --config 4 > /dev/null && echo "pmc4 ok"
