@@ -15,20 +15,38 @@
 
 namespace brb_digest {
 
-template <class Alg, int WAVES, int P, int BPS, bool OUT_ALIGNED>
+// Group assignment as in digest_line.h: static (wave w takes groups w, w + W_total, ...) or, with
+// DYN, workgroup b owns groups b, b + G, ... and its waves take them from an LDS ticket counter (the
+// older wave of a SIMD wins the issue arbitration, so a static split leaves the younger waves
+// running alone at the end).  DYN needs a ring of 2: each slot remembers the group of its stage.
+template <class Alg, int WAVES, int P, int BPS, bool OUT_ALIGNED, bool NT = false, bool DYN = false>
 __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
                                                                        uint64_t n_rec, uint8_t *__restrict__ out)
 {
-    using SG = brb_dma::Stager<BPS>;
+    static_assert(!DYN || P == 2, "ticketed groups are implemented for a ring of 2");
+    using SG = brb_dma::Stager<BPS, NT>;
     __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * P * SG::SLOT];
+    __shared__ uint32_t next_ticket;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
     const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
     const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
-    if (wave0 >= n_groups)
+    if (DYN) {
+        if (threadIdx.x == 0)
+            next_ticket = WAVES;                               // tickets 0 .. WAVES-1: one per wave
+        __syncthreads();
+    }
+    auto take = [&]() -> uint64_t {
+        uint32_t tk = 0;
+        if (lane == 0)
+            tk = __hip_atomic_fetch_add(&next_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tk = __builtin_amdgcn_readfirstlane(tk);
+        return uint64_t(blockIdx.x) + uint64_t(tk) * gridDim.x;
+    };
+    const uint64_t g0 = DYN ? uint64_t(blockIdx.x) + uint64_t(wv) * gridDim.x : wave0;
+    if (g0 >= n_groups)
         return;
-    const uint32_t my_groups = uint32_t((n_groups - wave0 + wstride - 1) / wstride);
 
     uint8_t *my = ring + wv * (P * SG::SLOT);
     const uint32_t lds_base = uint32_t(reinterpret_cast<uintptr_t>(my));
@@ -37,55 +55,66 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
     const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
     const uint32_t nblk = nfull + (t ? 1 : 0);                // blocks holding record bytes (>= 1)
     const uint32_t nstage = (nblk + BPS - 1) / BPS;           // stages per group
-    const uint32_t total = my_groups * nstage;                // stages of this wave
     const bool fast = rec_len >= 64 * BPS;                    // inst_offset form of the issue
-    const uint64_t grp_step = wstride * 64 * rec_len;         // bytes between this wave's groups
 
     // ---- issue cursor: runs P-1 stages ahead of the compute cursor, across group boundaries.
     // The descriptor base points at the stage being issued and num_records at the bytes left to
     // the end of the batch, so the range check zeroes exactly the bytes past the batch end.
-    uint64_t is_rec = wave0 * 64;                             // first record of the issuing group
-    uint64_t is_left = (n_rec - is_rec) * rec_len;
-    const uint8_t *is_base = data + is_rec * rec_len;
+    uint64_t is_g = g0;                                        // group of the next stage to issue
+    uint64_t is_left = (n_rec - g0 * 64) * rec_len;
+    const uint8_t *is_base = data + g0 * 64 * rec_len;
     uint32_t is_stage = 0, is_slot = lds_base;
+    uint32_t pending = 0;                                      // stages issued, not yet hashed
+    uint64_t slot_g0 = g0, slot_g1 = g0;                       // DYN: group of the stage in each slot
     SG sg;
-    sg.init(rec_len, uint32_t(n_rec - is_rec < 64 ? n_rec - is_rec : 64), lane, fast);
+    sg.init(rec_len, uint32_t(n_rec - g0 * 64 < 64 ? n_rec - g0 * 64 : 64), lane, fast);
     brb_dma::v4i rs = brb_dma::make_rsrc(is_base, is_left);
-    auto issue_next = [&]() {
+    auto issue_next = [&]() {                                  // precondition: is_g < n_groups
         if (fast)
             sg.issue_fast(rs, is_slot);
         else
             sg.issue_slow(rs, is_slot);
+        if (DYN) {
+            if (is_slot == lds_base)
+                slot_g0 = is_g;
+            else
+                slot_g1 = is_g;
+        }
+        ++pending;
         is_slot = is_slot == lds_last ? lds_base : is_slot + SG::SLOT;
         if (++is_stage < nstage) {
             is_base += SG::S;
             is_left -= SG::S;
         } else {                                              // this wave's next group
             is_stage = 0;
-            is_rec += wstride * 64;
-            is_base += grp_step - uint64_t(nstage - 1) * SG::S;
-            is_left = is_rec < n_rec ? (n_rec - is_rec) * rec_len : 0;
-            if (is_rec < n_rec && n_rec - is_rec < 64)
-                sg.group_offsets(rec_len, uint32_t(n_rec - is_rec), fast);
+            is_g = DYN ? take() : is_g + wstride;
+            const uint64_t r0 = is_g * 64;
+            is_base = data + r0 * rec_len;
+            is_left = is_g < n_groups ? (n_rec - r0) * rec_len : 0;
+            if (is_g < n_groups && n_rec - r0 < 64)
+                sg.group_offsets(rec_len, uint32_t(n_rec - r0), fast);
         }
         rs = brb_dma::make_rsrc(is_base, is_left);
     };
 #pragma unroll
     for (int i = 0; i < P - 1; i++)
-        if (uint32_t(i) < total)
+        if (is_g < n_groups)
             issue_next();
 
     typename Alg::State st = Alg::iv();
     uint32_t w[16];
-    uint64_t rb = wave0 * 64;                                  // compute cursor: first record of group
+    uint64_t rb = g0 * 64;                                     // compute cursor: first record of group
     uint32_t cs = 0, slot = lds_base;
-    for (uint32_t s = 0; s < total; s++) {
-        if (s + P - 1 < total) {
+    while (pending) {
+        if (is_g < n_groups) {
             issue_next();
             brb_dma::wait_vmcnt<SG::NI * (P - 1)>();
         } else {
             brb_dma::wait_vmcnt<0>();
         }
+        --pending;
+        if (DYN)
+            rb = (slot == lds_base ? slot_g0 : slot_g1) * 64;
         const uint8_t *sp = my + (slot - lds_base);
         slot = slot == lds_last ? lds_base : slot + SG::SLOT;
         const uint32_t b0 = cs * BPS;
@@ -145,7 +174,8 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
             Alg::template store<OUT_ALIGNED>(out, r, st);
         st = Alg::iv();
         cs = 0;
-        rb += wstride * 64;
+        if (!DYN)
+            rb += wstride * 64;
     }
 }
 
@@ -160,28 +190,30 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
                             hipStream_t s)
 {
     // Shapes measured with tools/mb/md5_ab.hip (interleaved, one process):
-    //  * records > 64 B: 128-byte stages, ring of 2 (16 KiB per wave, 64 KiB per 4-wave workgroup,
-    //    2 workgroups per CU): 1 Mi x 1500 B 335 us vs 388 us with 64-byte stages;
+    //  * records > 64 B at any alignment: 128-byte stages, ring of 2 (16 KiB per wave): 1 Mi x
+    //    1500 B 335 us vs 388 us with 64-byte stages;
     //  * records <= 64 B (one block + padding): 64-byte stages, ring of 2, 4 workgroups per CU.
     // Persistent beyond the resident grid (waves loop over groups of 64 records).
     constexpr int W = 4;
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs_needed = (groups + W - 1) / W;
-    // More than one wave per SIMD and 4-byte record bases with an odd dword stride (the record
-    // offsets within a line then take every dword position, so the window's ds_read_b32 are free of
-    // bank conflicts): line-aligned staging, digest_line.h.  1 Mi x 1500 B: 332 -> 305 us
-    // (tools/mb/md5_ab.hip).  At one wave per SIMD (cfg2) the two are even and this kernel stays.
-    if (groups > 1024 && line_supported(data, rec_len) && ((rec_len >> 2) & 1))
+    // 4-byte record bases and lengths over 64 B: line-aligned staging, digest_line.h (every line
+    // is read once; no 128-byte piece straddles two lines).  1 Mi x 1500 B: 343 -> 300 us,
+    // cfg2: 25.3 -> 24.9 us (tools/mb/md5_ab.hip).
+    if (line_supported(data, rec_len))
         return launch_fixed_line<Alg>(data, rec_len, n_rec, out, out_al, s);
     if (rec_len > 64) {
-        const unsigned g = unsigned(wgs_needed < 512 ? wgs_needed : 512);
+        // one 8-wave workgroup per CU (two waves per SIMD, 128 KiB of LDS), persistent, groups
+        // handed out by tickets, 128-byte stages, ring of 2
+        const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
         if (out_al)
-            digest_fixed_dma_kernel<Alg, W, 2, 2, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+            digest_fixed_dma_kernel<Alg, 8, 2, 2, true, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
         else
-            digest_fixed_dma_kernel<Alg, W, 2, 2, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+            digest_fixed_dma_kernel<Alg, 8, 2, 2, false, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
     } else {
-        // 4 workgroups per CU (32 KiB each): 1 Mi x 64 B = 16 384 groups = exactly 4 per wave, no
-        // tail imbalance; 23.2 us vs 23.7 us for a ring of 3 at 3 workgroups per CU (warm, md5_ab)
+        // 4 workgroups per CU (32 KiB each), static groups: 1 Mi x 64 B = 16 384 groups = exactly 4
+        // per wave.  Measured (md5_ab, 1 Mi x 64 B): 24.6 us; one 16-wave workgroup per CU with
+        // tickets 25.3 us; a ring of 3 at 3 workgroups per CU 26.1 us.
         const unsigned g = unsigned(wgs_needed < 1024 ? wgs_needed : 1024);
         if (out_al)
             digest_fixed_dma_kernel<Alg, W, 2, 1, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);

@@ -26,6 +26,12 @@
 
 #include "dma_stage.h"
 
+// Diagnostic hooks (tools/mb/line_probe.hip defines them; empty in the product build).
+#ifndef BRB_LINE_PROBE
+#define BRB_LINE_PROBE_DECL
+#define BRB_LINE_PROBE(ev) ((void)0)
+#endif
+
 namespace brb_digest {
 
 // Padding, digest and store of one group: the record's tail block (if any) is window half
@@ -66,20 +72,43 @@ BRB_DEV void line_finish(typename Alg::State &st, const uint32_t (&w0)[16], cons
         Alg::template store<OUT_ALIGNED>(out, r, st);
 }
 
-// launch_bounds min 2 waves per SIMD: two 4-wave workgroups per CU (64 KiB of LDS each).
-template <class Alg, int WAVES, bool OUT_ALIGNED>
-__global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data, uint32_t rec_len,
-                                                                     uint64_t n_rec, uint8_t *__restrict__ out)
+// Group assignment.  Static (DYN = false): wave w of the grid takes groups w, w + W_total, ...
+// Dynamic (DYN = true): workgroup b owns groups b, b + G, b + 2G, ... (G = gridDim.x) and its waves
+// take them one at a time from an LDS ticket counter.  Why: with two waves per SIMD the older wave
+// wins the issue arbitration, so under a static split the first workgroup of every CU finished its
+// share at ~190 us and the second one ran alone (at the lone-wave issue rate) until ~300 us
+// (1 Mi x 1500 B, tools/mb/line_probe.hip); with tickets the faster wave simply takes more groups.
+// launch_bounds: two waves per SIMD (4-wave workgroups: two per CU, 64 KiB of LDS each; 8-wave
+// workgroups: one per CU, 128 KiB).
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool NT = false, bool DYN = false>
+__global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data,
+                                                                             uint32_t rec_len, uint64_t n_rec,
+                                                                             uint8_t *__restrict__ out)
 {
     constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
     __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
+    __shared__ uint32_t next_ticket;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
     const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
     const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
-    if (wave0 >= n_groups)
+    if (DYN) {
+        if (threadIdx.x == 0)
+            next_ticket = WAVES;                               // tickets 0 .. WAVES-1: one per wave
+        __syncthreads();
+    }
+    auto take = [&]() -> uint64_t {                            // DYN: the next group of this workgroup
+        uint32_t tk = 0;
+        if (lane == 0)
+            tk = __hip_atomic_fetch_add(&next_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tk = __builtin_amdgcn_readfirstlane(tk);
+        return uint64_t(blockIdx.x) + uint64_t(tk) * gridDim.x;
+    };
+    uint64_t g = DYN ? uint64_t(blockIdx.x) + uint64_t(wv) * gridDim.x : wave0;
+    if (g >= n_groups)
         return;
+    uint64_t gn = DYN ? take() : g + wstride;                  // the group after g
 
     const uint32_t my_off = wv * 2 * SLOT;                     // slot 0; slot 1 = my_off + SLOT (bit 13 clear)
     const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + my_off;
@@ -112,19 +141,24 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         const uint64_t base = gline + 128ull * k;
         const brb_dma::v4i rs =
             brb_dma::make_rsrc(reinterpret_cast<const uint8_t *>(base), end_line > base ? end_line - base : 0);
+#define BRB_LINE_DMA(POL)                                                  \
+    asm volatile("s_mov_b32 %0, m0\n\t"                                     \
+                 "s_mov_b32 m0, %3\n\t"                                     \
+                 "s_nop 0\n\t"                                              \
+                 "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\t"       \
+                 "s_mov_b32 m0, %0"                                          \
+                 : "=&s"(keep)                                               \
+                 : "v"(vq[q]), "s"(rs), "s"(lds0 + slot * SLOT + 1024u * q)  \
+                 : "memory")
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             uint32_t keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\t"
-                "s_mov_b32 m0, %3\n\t"
-                "s_nop 0\n\t"
-                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(vq[q]), "s"(rs), "s"(lds0 + slot * SLOT + 1024u * q)
-                : "memory");
+            if constexpr (NT)
+                BRB_LINE_DMA("nt ");
+            else
+                BRB_LINE_DMA("");
         }
+#undef BRB_LINE_DMA
     };
 
     // ---- read side: window dword i of this lane -> LDS offset, for lines (k-1, k) in slots
@@ -156,7 +190,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // window in VGPRs before its slot is refilled
     };
 
-    uint64_t g = wave0;
+    BRB_LINE_PROBE_DECL
+    BRB_LINE_PROBE(0);
     dma_setup(g);
     issue(0, 0);
     issue(1, 1);
@@ -168,15 +203,17 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         // one compress site per block (the code must stay small: one wave per SIMD runs out of
         // the shared instruction cache at once when the loop body is unrolled)
         for (uint32_t k = 1; k <= K; k++) {
+            BRB_LINE_PROBE(1);
             brb_dma::wait_vmcnt<0>();
             if (k & 1)
                 read_window(ae);
             else
                 read_window(ao);
+            BRB_LINE_PROBE(2);
             if (k < K) {
                 issue((k + 1) & 1, k + 1);
-            } else if (g + wstride < n_groups) {
-                dma_setup(g + wstride);
+            } else if (gn < n_groups) {
+                dma_setup(gn);
                 issue(0, 0);
                 issue(1, 1);
             }
@@ -187,11 +224,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
                 Alg::compress(st, w1);
         }
         line_finish<Alg, OUT_ALIGNED>(st, w0, w1, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
-        g += wstride;
+        g = gn;
         if (g >= n_groups)
             break;
+        gn = DYN ? take() : g + wstride;
         win_setup(g);
     }
+    BRB_LINE_PROBE(3);
 }
 
 // Line-aligned staging needs 4-byte record bases (the window shift is whole dwords).
@@ -201,18 +240,33 @@ inline bool line_supported(const uint8_t *data, uint32_t rec_len)
            uint64_t(rec_len) * 64 + 256 < (uint64_t(1) << 31);
 }
 
+inline unsigned device_cu_count()
+{
+    static const unsigned n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return unsigned(c);
+    }();
+    return n;
+}
+
+// One 8-wave workgroup per CU (128 KiB of LDS), persistent, groups handed out by tickets (DYN), DMA
+// with the non-temporal policy (every line is read exactly once).  Measured with
+// tools/mb/md5_ab.hip, MD5, medians of 20-launch bursts:
+//   1 Mi x 1500 B: 316 us static 4-wave workgroups -> 300 us (read floor of the same bytes: 261 us nt)
+//   cfg2 65 536 x 1500 B: 25.3 us (record-relative 128-byte stages) -> 24.9 us
 template <class Alg>
 hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
                              hipStream_t s)
 {
-    constexpr int W = 4;
+    constexpr int W = 8;
     const uint64_t groups = (n_rec + 63) / 64;
-    const uint64_t wgs_needed = (groups + W - 1) / W;
-    const unsigned g = unsigned(wgs_needed < 512 ? wgs_needed : 512);   // 2 workgroups per CU, persistent
+    const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
     if (out_al)
-        digest_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+        digest_line_kernel<Alg, W, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
     else
-        digest_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+        digest_line_kernel<Alg, W, false, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
     return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@
 // the batch, each lane's record row + granule a 32-bit voffset: staging costs no VALU per stage,
 // and the hardware range check (voffset + inst_offset against num_records) returns zeros for bytes
 // past the batch end instead of faulting.
+//
+// NT = true sets the non-temporal policy (nt) on the DMA: the records are read exactly once.
 #pragma once
 
 #include "brb_gpu_common.h"
@@ -39,7 +41,7 @@ BRB_DEV v4i make_rsrc(const uint8_t *base, uint64_t extent)
     return r;
 }
 
-template <int BPS>
+template <int BPS, bool NT = false>
 struct Stager {
     static constexpr int S = 64 * BPS;          // bytes of one record per stage
     static constexpr int G = S / 16;            // 16-byte granules per record row
@@ -79,42 +81,52 @@ struct Stager {
     // DMA) is compiler-reserved, so it is saved and restored inside the statement.
     BRB_DEV void issue_fast(const v4i &rsrc, uint32_t slot_lds) const
     {
+#define BRB_DMA_FAST(POL)                                                                              \
+    asm volatile("s_mov_b32 %0, m0\n\t"                                                                 \
+                 "s_mov_b32 m0, %6\n\t"                                                                 \
+                 "s_nop 0\n\t"                                                                          \
+                 "buffer_load_dwordx4 %1, %5, 0 offen " POL "lds\n\t"                                   \
+                 "buffer_load_dwordx4 %2, %5, 0 offen offset:1024 " POL "lds\n\t"                       \
+                 "buffer_load_dwordx4 %3, %5, 0 offen offset:2048 " POL "lds\n\t"                       \
+                 "buffer_load_dwordx4 %4, %5, 0 offen offset:3072 " POL "lds\n\t"                       \
+                 "s_mov_b32 m0, %0"                                                                      \
+                 : "=&s"(keep)                                                                           \
+                 : "v"(vq[4 * h]), "v"(vq[4 * h + 1]), "v"(vq[4 * h + 2]), "v"(vq[4 * h + 3]), "s"(rsrc), \
+                   "s"(slot_lds + 4096u * h)                                                             \
+                 : "memory")
 #pragma unroll
         for (int h = 0; h < BPS; h++) {
             uint32_t keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\t"
-                "s_mov_b32 m0, %6\n\t"
-                "s_nop 0\n\t"
-                "buffer_load_dwordx4 %1, %5, 0 offen lds\n\t"
-                "buffer_load_dwordx4 %2, %5, 0 offen offset:1024 lds\n\t"
-                "buffer_load_dwordx4 %3, %5, 0 offen offset:2048 lds\n\t"
-                "buffer_load_dwordx4 %4, %5, 0 offen offset:3072 lds\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(vq[4 * h]), "v"(vq[4 * h + 1]), "v"(vq[4 * h + 2]), "v"(vq[4 * h + 3]), "s"(rsrc),
-                  "s"(slot_lds + 4096u * h)
-                : "memory");
+            if constexpr (NT)
+                BRB_DMA_FAST("nt ");
+            else
+                BRB_DMA_FAST("");
         }
+#undef BRB_DMA_FAST
     }
 
     // Same, one M0 write per instruction (strides below 128, where the inst_offset trick would
     // need negative voffsets).
     BRB_DEV void issue_slow(const v4i &rsrc, uint32_t slot_lds) const
     {
+#define BRB_DMA_SLOW(POL)                                                \
+    asm volatile("s_mov_b32 %0, m0\n\t"                                   \
+                 "s_mov_b32 m0, %3\n\t"                                   \
+                 "s_nop 0\n\t"                                            \
+                 "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\t"     \
+                 "s_mov_b32 m0, %0"                                        \
+                 : "=&s"(keep)                                             \
+                 : "v"(vq[q]), "s"(rsrc), "s"(slot_lds + 1024u * q)        \
+                 : "memory")
 #pragma unroll
         for (int q = 0; q < NI; q++) {
             uint32_t keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\t"
-                "s_mov_b32 m0, %3\n\t"
-                "s_nop 0\n\t"
-                "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(vq[q]), "s"(rsrc), "s"(slot_lds + 1024u * q)
-                : "memory");
+            if constexpr (NT)
+                BRB_DMA_SLOW("nt ");
+            else
+                BRB_DMA_SLOW("");
         }
+#undef BRB_DMA_SLOW
     }
 
     // Read this lane's block j (0 <= j < BPS) of the stage in `slot` as 16 little-endian words.

@@ -28,9 +28,11 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
     src.fetch(c);
     const uint64_t pos = 64 * b;
     if (pos + 64 <= F) {
+        uint32_t ks[16];
+        g.words(ks);
 #pragma unroll
         for (int i = 0; i < 16; i++) {
-            pt[i] = c[i] ^ g.next4();
+            pt[i] = c[i] ^ ks[i];
             snk.put(pt[i]);
         }
     } else {
@@ -71,9 +73,11 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
         src.fetch(c);
         const uint64_t pos = 64 * b;
         if (pos + 64 <= len) {
+            uint32_t ks[16];
+            g.words(ks);
 #pragma unroll
             for (int i = 0; i < 16; i++)
-                snk.put(c[i] ^ g.next4());
+                snk.put(c[i] ^ ks[i]);
         } else {
 #pragma unroll
             for (int i = 0; i < 16; i++) {
@@ -124,20 +128,47 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
     for (uint64_t b = 0; b < nblk; b++) {
         uint32_t m[16], rw[16];
         src.fetch(rw);
+        // frame chunks 16b + 7 .. 16b + 22 (payload words 16b .. 16b + 15; word 0 lives in the
+        // header chunk 7): when all of them lie inside the frame, their keystream is one run
+        if (4 * (16 * b + 23) <= F) {
+            uint32_t ks[16];
+            if (b == 0) {
+                uint32_t k15[15];
+                g.words(k15);
 #pragma unroll
-        for (uint32_t i = 0; i < 16; i++) {
-            const uint64_t w = 16 * b + i;
-            const uint32_t raw = rw[i];
-            if (w == 0) {
-                first = raw;
+                for (int i = 0; i < 15; i++)
+                    ks[i + 1] = k15[i];
+                ks[0] = 0;
             } else {
-                // frame chunk w + 7 = payload bytes 4w - 2 .. 4w + 1
-                const uint64_t fb = 4 * (w + 7);
-                if (fb < F)
-                    snk.put(__builtin_amdgcn_alignbit(raw, prev, 16) ^ g.next_n(clamp4(F - fb)));
+                g.words(ks);
             }
-            prev = raw;
-            m[i] = md5_pad_word(raw, w, len, nw);
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                const uint64_t w = 16 * b + i;
+                const uint32_t raw = rw[i];
+                if (w == 0)
+                    first = raw;
+                else
+                    snk.put(__builtin_amdgcn_alignbit(raw, prev, 16) ^ ks[i]);
+                prev = raw;
+                m[i] = md5_pad_word(raw, w, len, nw);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                const uint64_t w = 16 * b + i;
+                const uint32_t raw = rw[i];
+                if (w == 0) {
+                    first = raw;
+                } else {
+                    // frame chunk w + 7 = payload bytes 4w - 2 .. 4w + 1
+                    const uint64_t fb = 4 * (w + 7);
+                    if (fb < F)
+                        snk.put(__builtin_amdgcn_alignbit(raw, prev, 16) ^ g.next_n(clamp4(F - fb)));
+                }
+                prev = raw;
+                m[i] = md5_pad_word(raw, w, len, nw);
+            }
         }
         md5_compress(st, m);
     }

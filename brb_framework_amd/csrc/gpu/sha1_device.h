@@ -17,10 +17,14 @@ BRB_DEV Sha1State sha1_iv()
     return Sha1State{0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
 }
 
-#define BRB_SHA1_CH(b, c, d) ((d) ^ ((b) & ((c) ^ (d))))
-#define BRB_SHA1_PAR(b, c, d) ((b) ^ (c) ^ (d))
-#define BRB_SHA1_MAJ(b, c, d) (((b) & (c)) | ((d) & ((b) | (c))))
-#define BRB_SHA1_W(i) (w[(i) & 15] = rotl<1>(w[((i) + 13) & 15] ^ w[((i) + 8) & 15] ^ w[((i) + 2) & 15] ^ w[(i) & 15]))
+// Each round function is one v_bitop3_b32 (truth table indexed by b << 2 | c << 1 | d).  Written
+// with the builtin: hipcc lowers the plain C forms of Parity and Maj to two ops (xor + xor,
+// bfi + xor), and the schedule's four-way xor to three xors.
+#define BRB_SHA1_CH(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xCA)
+#define BRB_SHA1_PAR(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)
+#define BRB_SHA1_MAJ(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xE8)
+#define BRB_SHA1_W(i) \
+    (w[(i) & 15] = rotl<1>(__builtin_amdgcn_bitop3_b32(w[((i) + 13) & 15], w[((i) + 8) & 15], w[((i) + 2) & 15], 0x96) ^ w[(i) & 15]))
 // round with the roles of (a..e) rotated by the caller, as the reference's R0..R4 macros do
 #define BRB_SHA1_R(F, K, v, x, y, z, u, wi)                    \
     do {                                                       \

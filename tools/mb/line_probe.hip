@@ -1,0 +1,159 @@
+// line_probe.hip -- where does a wave of the line-aligned digest kernel spend its time?
+// Per wave: shader-clock and 100 MHz real-time stamps at start and end, and the shader clocks spent
+// waiting for its LDS-DMA lines (s_waitcnt vmcnt + the window read).  Prints the clock, the start /
+// end skew over waves and the wait fraction.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../brb_framework_amd/csrc/gpu line_probe.hip -o lprobe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+__device__ uint64_t *g_probe;
+__device__ inline uint64_t pr_clk()
+{
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+__device__ inline uint64_t pr_rt()
+{
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define BRB_LINE_PROBE 1
+#define BRB_LINE_PROBE_DECL uint64_t pr_c0 = 0, pr_r0 = 0, pr_tw = 0, pr_wait = 0;
+#define BRB_LINE_PROBE(ev)                                                              \
+    do {                                                                                \
+        if ((ev) == 0) { pr_c0 = pr_clk(); pr_r0 = pr_rt(); }                           \
+        if ((ev) == 1) pr_tw = pr_clk();                                                \
+        if ((ev) == 2) pr_wait += pr_clk() - pr_tw;                                     \
+        if ((ev) == 3 && lane == 0) {                                                   \
+            uint64_t *o = g_probe + 5 * wave0;                                          \
+            o[0] = pr_c0; o[1] = pr_clk(); o[2] = pr_r0; o[3] = pr_rt(); o[4] = pr_wait;\
+        }                                                                               \
+    } while (0)
+
+#include "digest_line.h"
+#include "md5_device.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+struct AlgLit {
+    using State = Md5State;
+    static BRB_DEV State iv() { return md5_iv(); }
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16]) { md5_compress(st, w); }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t t, uint64_t len) { md5_finish(st, w, t, len); }
+    static BRB_DEV void pad_only(State &st, uint64_t len) { md5_pad_only(st, len); }
+    template <bool A> static BRB_DEV void store(uint8_t *out, uint64_t r, const State &st)
+    { reinterpret_cast<uint4 *>(out)[r] = make_uint4(st.a, st.b, st.c, st.d); }
+};
+struct AlgNull : AlgLit {
+    static BRB_DEV void compress(State &st, uint32_t (&w)[16])
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) x ^= w[i];
+        st.a ^= x;
+    }
+    static BRB_DEV void finish(State &st, uint32_t (&w)[16], uint32_t, uint64_t) { st.b ^= w[0]; }
+    static BRB_DEV void pad_only(State &st, uint64_t len) { st.b ^= uint32_t(len); }
+};
+
+using Kern = void (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *);
+
+static double pct(std::vector<double> v, double p)
+{
+    std::sort(v.begin(), v.end());
+    return v[size_t(p * (v.size() - 1))];
+}
+
+int main(int argc, char **argv)
+{
+    const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 65536;
+    const uint32_t L = argc > 2 ? atoi(argv[2]) : 1500;
+    const int nrot = std::max<int>(2, int(700e6 / double(n * L)) + 1);
+    std::vector<uint8_t> h(n * L);
+    uint64_t x = 7;
+    for (auto &c : h) { x = x * 6364136223846793005ull + 1442695040888963407ull; c = uint8_t(x >> 56); }
+    std::vector<uint8_t *> d(nrot);
+    for (auto &p : d) { CK(hipMalloc(&p, n * L + 8192)); CK(hipMemcpy(p, h.data(), n * L, hipMemcpyHostToDevice)); }
+    uint8_t *o;
+    CK(hipMalloc(&o, n * 16));
+    const uint64_t groups = (n + 63) / 64;
+    uint64_t *pr;
+    CK(hipMalloc(&pr, 4096 * 5 * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
+    struct V { const char *name; Kern k; };
+    struct VG { const char *name; Kern k; int waves; };
+    VG vs[] = {{"LINE md5", brb_digest::digest_line_kernel<AlgLit, 4, true>, 4},
+              {"LINE md5 nt dyn8", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE md5 nt dyn4", brb_digest::digest_line_kernel<AlgLit, 4, true, true, true>, 4},
+              {"LINE md5 nt", brb_digest::digest_line_kernel<AlgLit, 4, true, true>, 4},
+              {"LINE dma-only nt", brb_digest::digest_line_kernel<AlgNull, 4, true, true>, 4}};
+    int it = 0;
+    for (auto &v : vs) {
+        // 4-wave workgroups: 2 per CU; 8-wave (dyn): one per CU, groups strided over the grid
+        const unsigned grid = v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, 512))
+                                           : unsigned(std::min<uint64_t>(groups, 256));
+        const uint64_t waves = std::min<uint64_t>(uint64_t(grid) * v.waves, groups);
+        const unsigned bs = 64 * v.waves;
+        // warm up >= 0.5 s (clocks), then probe one launch out of a back-to-back burst
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        float tot = 0;
+        while (tot < 500.f) {
+            hipEventRecord(a);
+            for (int i = 0; i < 50; i++) hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+            hipEventRecord(b);
+            CK(hipEventSynchronize(b));
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            tot += ms;
+        }
+        for (int i = 0; i < 9; i++) hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+        CK(hipMemsetAsync(pr, 0, 4096 * 5 * 8));
+        hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> all(4096 * 5), hp;
+        CK(hipMemcpy(all.data(), pr, all.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> widx;
+        for (uint64_t w = 0; w < 4096; w++)
+            if (all[5 * w + 1]) {
+                widx.push_back(w);
+                hp.insert(hp.end(), &all[5 * w], &all[5 * w + 5]);
+            }
+        (void)waves;
+        const uint64_t nw = widx.size();
+        uint64_t r0 = ~0ull, r1 = 0;
+        for (uint64_t w = 0; w < nw; w++) { r0 = std::min(r0, hp[5 * w + 2]); r1 = std::max(r1, hp[5 * w + 3]); }
+        std::vector<double> mhz, st, en, dur, wf;
+        for (uint64_t w = 0; w < nw; w++) {
+            const uint64_t *q = &hp[5 * w];
+            const double rt = double(q[3] - q[2]) * 10.0;  // ns (100 MHz)
+            mhz.push_back(double(q[1] - q[0]) / (rt * 1e-3));
+            st.push_back(double(q[2] - r0) * 10.0 / 1000.0);
+            en.push_back(double(q[3] - r0) * 10.0 / 1000.0);
+            dur.push_back(rt / 1000.0);
+            wf.push_back(double(q[4]) / double(q[1] - q[0]));
+        }
+        {   // per-XCD (blockIdx % 8) mean end time, and a histogram of end times
+            double sx[8] = {0}; int cx[8] = {0};
+            for (uint64_t w = 0; w < nw; w++) { sx[(widx[w] / v.waves) % 8] += en[w]; cx[(widx[w] / v.waves) % 8]++; }
+            printf("  waves %llu, per-XCD mean end us:", (unsigned long long)nw);
+            for (int i = 0; i < 8; i++) printf(" %.1f", sx[i] / cx[i]);
+            printf("\n  end pcts:");
+            for (double q : {0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 0.95, 0.99, 1.0}) printf(" p%g=%.1f", q * 100, pct(en, q));
+            std::vector<double> by_slot[2];
+            for (uint64_t w = 0; w < nw; w++) by_slot[widx[w] / 1024 % 2].push_back(en[w]);
+            printf("\n  WG<256 end p50 %.1f p90 %.1f | WG>=256 end p50 %.1f p90 %.1f\n", pct(by_slot[0], .5), pct(by_slot[0], .9),
+                   by_slot[1].empty() ? 0.0 : pct(by_slot[1], .5), by_slot[1].empty() ? 0.0 : pct(by_slot[1], .9));
+        }
+        printf("%-18s n=%llu L=%u  span %.2f us | clock MHz p50 %.0f | start us p0 %.2f p50 %.2f p100 %.2f | end us p0 %.2f p50 %.2f p100 %.2f | wave us p50 %.2f | wait frac p10 %.2f p50 %.2f p90 %.2f\n",
+               v.name, (unsigned long long)n, L, double(r1 - r0) * 10.0 / 1000.0, pct(mhz, .5), pct(st, 0), pct(st, .5), pct(st, 1),
+               pct(en, 0), pct(en, .5), pct(en, 1), pct(dur, .5), pct(wf, .1), pct(wf, .5), pct(wf, .9));
+    }
+    return 0;
+}
