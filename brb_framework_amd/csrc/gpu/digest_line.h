@@ -124,23 +124,68 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // ---- issue side: DMA lane j of instruction q stages granule j % 8 of row 8q + j / 8
     uint32_t vq[8];
     uint64_t gline = 0;                                        // first line of the issuing group
+    uint64_t gleft = 0;                                        // bytes from gline to end_line
+    // fastq: DMA q carries the instruction offset 1024 (q % 4), which lands in the LDS address as
+    // well, so one M0 write serves four DMAs; the voffset is lowered by the same amount.  Needs
+    // every voffset >= 3072 where q % 4 == 3: full groups and records of at least 160 bytes.
+    bool fastq = false;
     auto dma_setup = [&](uint64_t g) {
         const uint64_t r0 = g * 64;
         const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
         const uint64_t a0 = dbase + r0 * rec_len;
         gline = a0 & ~uint64_t(127);
+        gleft = end_line - gline;
         const uint32_t o0 = uint32_t(a0) & 127;
+        fastq = last == 63 && rec_len >= 160;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const uint32_t row = 8 * q + (lane >> 3);
             const uint32_t rr = row < last ? row : last;
-            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row));
+            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row)) - (fastq ? 1024u * (q & 3) : 0u);
         }
     };
     auto issue = [&](uint32_t slot, uint32_t k) {              // line k of the issuing group -> slot
+        // descriptor of line k: base gline + 128 k, num_records = bytes left to end_line clamped to
+        // [0, 2^31 - 1], in 32-bit scalar ops (gfx950 has no 64-bit ordered scalar compare)
         const uint64_t base = gline + 128ull * k;
-        const brb_dma::v4i rs =
-            brb_dma::make_rsrc(reinterpret_cast<const uint8_t *>(base), end_line > base ? end_line - base : 0);
+        const int64_t left = int64_t(gleft) - int64_t(128u * k);
+        const int32_t lhi = int32_t(uint64_t(left) >> 32);
+        const uint32_t llo = uint32_t(left);
+        const uint32_t nrec = lhi < 0 ? 0u : (lhi > 0 || llo > 0x7FFFFFFFu) ? 0x7FFFFFFFu : llo;
+        brb_dma::v4i rs;
+        rs.x = int(uint32_t(base));
+        rs.y = int(uint32_t(base >> 32) & 0xFFFF);
+        rs.z = int(nrec);
+        rs.w = 0x00020000;
+        const uint32_t m = lds0 + slot * SLOT;
+        if (fastq) {
+#define BRB_LINE_DMA8(POL)                                                                      \
+    asm volatile("s_mov_b32 %0, m0\n\t"                                                          \
+                 "s_mov_b32 m0, %10\n\t"                                                         \
+                 "s_nop 0\n\t"                                                                   \
+                 "buffer_load_dwordx4 %1, %9, 0 offen " POL "lds\n\t"                            \
+                 "buffer_load_dwordx4 %2, %9, 0 offen offset:1024 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %3, %9, 0 offen offset:2048 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %4, %9, 0 offen offset:3072 " POL "lds\n\t"                \
+                 "s_mov_b32 m0, %11\n\t"                                                         \
+                 "s_nop 0\n\t"                                                                   \
+                 "buffer_load_dwordx4 %5, %9, 0 offen " POL "lds\n\t"                            \
+                 "buffer_load_dwordx4 %6, %9, 0 offen offset:1024 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %7, %9, 0 offen offset:2048 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %8, %9, 0 offen offset:3072 " POL "lds\n\t"                \
+                 "s_mov_b32 m0, %0"                                                               \
+                 : "=&s"(keep)                                                                    \
+                 : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "v"(vq[4]), "v"(vq[5]), "v"(vq[6]), \
+                   "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u)                                    \
+                 : "memory")
+            uint32_t keep;
+            if constexpr (NT)
+                BRB_LINE_DMA8("nt ");
+            else
+                BRB_LINE_DMA8("");
+#undef BRB_LINE_DMA8
+            return;
+        }
 #define BRB_LINE_DMA(POL)                                                  \
     asm volatile("s_mov_b32 %0, m0\n\t"                                     \
                  "s_mov_b32 m0, %3\n\t"                                     \
@@ -148,7 +193,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
                  "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\t"       \
                  "s_mov_b32 m0, %0"                                          \
                  : "=&s"(keep)                                               \
-                 : "v"(vq[q]), "s"(rs), "s"(lds0 + slot * SLOT + 1024u * q)  \
+                 : "v"(vq[q]), "s"(rs), "s"(m + 1024u * q)                   \
                  : "memory")
 #pragma unroll
         for (int q = 0; q < 8; q++) {
