@@ -31,10 +31,9 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
         uint32_t ks[16];
         g.words(ks);
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < 16; i++)
             pt[i] = c[i] ^ ks[i];
-            snk.put(pt[i]);
-        }
+        snk.put16(pt);
     } else {
 #pragma unroll
         for (int i = 0; i < 16; i++) {
@@ -77,7 +76,8 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
             g.words(ks);
 #pragma unroll
             for (int i = 0; i < 16; i++)
-                snk.put(c[i] ^ ks[i]);
+                ks[i] ^= c[i];
+            snk.put16(ks);
         } else {
 #pragma unroll
             for (int i = 0; i < 16; i++) {
@@ -142,16 +142,23 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
             } else {
                 g.words(ks);
             }
+            uint32_t ct[16];
 #pragma unroll
             for (uint32_t i = 0; i < 16; i++) {
                 const uint64_t w = 16 * b + i;
                 const uint32_t raw = rw[i];
                 if (w == 0)
                     first = raw;
-                else
-                    snk.put(__builtin_amdgcn_alignbit(raw, prev, 16) ^ ks[i]);
+                ct[i] = __builtin_amdgcn_alignbit(raw, prev, 16) ^ ks[i];
                 prev = raw;
                 m[i] = md5_pad_word(raw, w, len, nw);
+            }
+            if (b == 0) {
+#pragma unroll
+                for (int i = 1; i < 16; i++)
+                    snk.put(ct[i]);
+            } else {
+                snk.put16(ct);
             }
         } else {
 #pragma unroll
