@@ -19,20 +19,55 @@ BRB_DEV uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh)
     return __builtin_amdgcn_alignbit(hi, lo, sh);
 }
 
-// 16-byte load from a 4-byte-aligned global address (gfx950 runs in unaligned-access mode; the
-// compiler emits one global_load_dwordx4).
+// Global-memory accessors.  Pointers rebuilt from integers (byte offsets rounded to dwords) lose
+// their address space, and hipcc then emits FLAT instructions, which count in LGKM_CNT as well as
+// VM_CNT: every LDS wait of a kernel (the RC4 generator's) would also wait for its HBM loads and
+// stores.  These casts keep them global_load / global_store.
+#define BRB_GLOBAL __attribute__((address_space(1)))
+#define BRB_GPTR(T, p) ((BRB_GLOBAL T *)(uintptr_t)(p))
+typedef uint32_t brb_v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// 16-byte load from a 4-byte-aligned global address (gfx950 runs in unaligned-access mode; one
+// global_load_dwordx4).
 BRB_DEV uint4 ld16_a4(const uint8_t *p)
 {
-    uint4 v;
-    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 16);
-    return v;
+    const brb_v4u_a4 v = *BRB_GPTR(const brb_v4u_a4, p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+BRB_DEV void st16_a4(uint8_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    brb_v4u_a4 v;
+    v.x = a;
+    v.y = b;
+    v.z = c;
+    v.w = d;
+    *BRB_GPTR(brb_v4u_a4, p) = v;
 }
 
 BRB_DEV uint32_t ld4_a4(const uint8_t *p)
 {
-    uint32_t v;
-    __builtin_memcpy(&v, __builtin_assume_aligned(p, 4), 4);
-    return v;
+    return *BRB_GPTR(const uint32_t, p);
+}
+
+BRB_DEV uint32_t ldg(const uint32_t *p)
+{
+    return *BRB_GPTR(const uint32_t, p);
+}
+
+BRB_DEV void stg(uint32_t *p, uint32_t v)
+{
+    *BRB_GPTR(uint32_t, p) = v;
+}
+
+BRB_DEV uint32_t ldg8(const uint8_t *p)
+{
+    return *BRB_GPTR(const uint8_t, p);
+}
+
+BRB_DEV void stg8(uint8_t *p, uint32_t v)
+{
+    *BRB_GPTR(uint8_t, p) = uint8_t(v);
 }
 
 // Little-endian word i (bytes [4i, 4i+4)) of a message tail of `t` valid bytes (t < 64) followed by
@@ -64,9 +99,9 @@ BRB_DEV uint32_t word_any(const uint8_t *a, uint64_t len, uint64_t blk_off, uint
         const uintptr_t addr = reinterpret_cast<uintptr_t>(a) + o;
         const uintptr_t a0 = addr & ~uintptr_t(3);
         const uint32_t sh = uint32_t(addr & 3) * 8;
-        const uint32_t lo = *reinterpret_cast<const uint32_t *>(a0);
+        const uint32_t lo = ldg(reinterpret_cast<const uint32_t *>(a0));
         // the second dword is read only if it holds a byte of this word (sh != 0)
-        const uint32_t hi = sh ? *reinterpret_cast<const uint32_t *>(a0 + 4) : 0u;
+        const uint32_t hi = sh ? ldg(reinterpret_cast<const uint32_t *>(a0 + 4)) : 0u;
         return funnel(hi, lo, sh);
     }
     uint32_t v = 0;
@@ -74,7 +109,7 @@ BRB_DEV uint32_t word_any(const uint8_t *a, uint64_t len, uint64_t blk_off, uint
         const uint64_t ob = o + k;
         uint32_t byte = 0;
         if (ob < len)
-            byte = a[ob];
+            byte = ldg8(a + ob);
         else if (ob == len)
             byte = 0x80u;
         v |= byte << (8 * k);

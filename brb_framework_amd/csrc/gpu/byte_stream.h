@@ -24,13 +24,13 @@ struct Src {
         p = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
         sh = uint32_t(ad & 3) * 8;
         rem = n;
-        lo = n ? p[0] : 0u;
+        lo = n ? ldg(p) : 0u;
     }
 
     BRB_DEV uint32_t next()
     {
         const uint32_t o = sh >> 3;
-        const uint32_t hi = rem > 4 - o ? p[1] : 0u;     // the next dword holds a byte of the range
+        const uint32_t hi = rem > 4 - o ? ldg(p + 1) : 0u;     // the next dword holds a byte of the range
         uint32_t v = __builtin_amdgcn_alignbit(hi, lo, sh);
         if (rem < 4)
             v &= (1u << (8 * uint32_t(rem))) - 1u;
@@ -64,12 +64,12 @@ struct Snk {
     static BRB_DEV void part(uint32_t *q, uint32_t w, uint32_t lo, uint32_t hi)
     {
         if (lo == 0 && hi == 3) {
-            *q = w;
+            stg(q, w);
             return;
         }
         uint8_t *b = reinterpret_cast<uint8_t *>(q);
         for (uint32_t k = lo; k <= hi; k++)
-            b[k] = uint8_t(w >> (8 * k));
+            stg8(b + k, w >> (8 * k));
     }
 
     BRB_DEV void put(uint32_t v)
@@ -118,10 +118,8 @@ struct Snk {
             prev = v[k];
         }
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint4 x = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-            __builtin_memcpy(__builtin_assume_aligned(p + 4 * q, 4), &x, 16);
-        }
+        for (int q = 0; q < 4; q++)
+            st16_a4(reinterpret_cast<uint8_t *>(p + 4 * q), w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
         p += 16;
         carry = o ? (v[15] >> (32 - 8 * o)) : 0u;
         carry_n = o;
@@ -157,7 +155,7 @@ struct BlockSrc {
         } else {
 #pragma unroll
             for (int i = 0; i < 16; i++)
-                L[i] = base + i < ndw ? p[base + i] : 0u;
+                L[i] = base + i < ndw ? ldg(p + base + i) : 0u;
         }
     }
 
@@ -168,23 +166,21 @@ struct BlockSrc {
         sh = uint32_t(ad & 3) * 8;
         len = n;
         ndw = n ? ((ad & 3) + n + 3) / 4 : 0;
-        prev = ndw ? p[0] : 0u;
+        prev = ndw ? ldg(p) : 0u;
         nb = 0;
         load(0);
     }
 
-    // chunks of block nb; starts the load of block nb + 1
+    // chunks of block nb; starts the load of block nb + 1.  The block in flight is consumed BEFORE
+    // the next load is issued: the two load paths (whole block / guarded dwords) leave hipcc unsure
+    // of the pending count, and a wait placed after the new load would wait for it too (one HBM
+    // round trip per block: 98 -> 138 us for 65 536 RC4 streams of 1500 B).
     BRB_DEV void fetch(uint32_t (&c)[16])
     {
-        uint32_t cur[16];
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            cur[i] = L[i];
-        load(nb + 1);
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            c[i] = __builtin_amdgcn_alignbit(cur[i], i ? cur[i - 1] : prev, sh);
-        prev = cur[15];
+            c[i] = __builtin_amdgcn_alignbit(L[i], i ? L[i - 1] : prev, sh);
+        prev = L[15];
         const uint64_t pos = 64 * nb;
         if (pos + 64 > len) {
 #pragma unroll
@@ -194,6 +190,7 @@ struct BlockSrc {
             }
         }
         ++nb;
+        load(nb);
     }
 };
 

@@ -67,9 +67,10 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
     src.init(in + off, len);
     snk.init(out + off, len);
     const uint64_t nblk = (len + 63) >> 6;
-    for (uint64_t b = 0; b < nblk; b++) {
-        uint32_t c[16];
+    uint32_t c[16];
+    if (nblk)
         src.fetch(c);
+    for (uint64_t b = 0; b < nblk; b++) {
         const uint64_t pos = 64 * b;
         if (pos + 64 <= len) {
             uint32_t ks[16];
@@ -77,6 +78,10 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
 #pragma unroll
             for (int i = 0; i < 16; i++)
                 ks[i] ^= c[i];
+            // the next block is taken (and the one after it requested) before this block's stores
+            // go out, so the wait for it never includes them
+            if (b + 1 < nblk)
+                src.fetch(c);
             snk.put16(ks);
         } else {
 #pragma unroll

@@ -17,6 +17,7 @@
 using namespace brb_rc4;
 
 template <int MODE>   // 0 full, 1 gen only, 2 io only, 3 io only with 16-byte stores, 4 loads only
+// 5 product loop (put16, next block taken before the stores), 6 product loop without stores, 7 product loop without loads
 __global__ __launch_bounds__(256) void k(uint8_t *states, const uint8_t *in, uint8_t *out, uint32_t L, uint64_t n, uint32_t *sink)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -39,6 +40,35 @@ __global__ __launch_bounds__(256) void k(uint8_t *states, const uint8_t *in, uin
     uint4 *o16 = reinterpret_cast<uint4 *>(out + off);
     uint32_t acc = 0;
     const uint64_t nblk = L / 64;
+    if (MODE >= 5) {
+        uint32_t c[16];
+        if (MODE == 7) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) c[i] = 0x3C3C3C3Cu + i;
+        } else {
+            src.fetch(c);
+        }
+        for (uint64_t b = 0; b < nblk; b++) {
+            uint32_t ks[16];
+            g.words(ks);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                ks[i] ^= c[i];
+            if (MODE != 7 && b + 1 < nblk)
+                src.fetch(c);
+            if (MODE == 6) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) acc ^= ks[i];
+            } else {
+                snk.put16(ks);
+            }
+        }
+        snk.flush();
+        g.store(state);
+        if (acc == 0x12345678u)
+            sink[0] = acc;
+        return;
+    }
     for (uint64_t b = 0; b < nblk; b++) {
         uint32_t c[16], ks[16];
         if (MODE != 1)
@@ -95,7 +125,7 @@ int main()
     CK(hipMemcpy(st, h.data(), h.size(), hipMemcpyHostToDevice));
     CK(hipMemset(in, 0x3C, n * L));
     struct V { const char *name; void (*f)(uint8_t *, const uint8_t *, uint8_t *, uint32_t, uint64_t, uint32_t *); } vs[] = {
-        {"full", k<0>}, {"gen only", k<1>}, {"io only", k<2>}, {"io 16B st", k<3>}, {"loads only", k<4>}};
+        {"full", k<0>}, {"gen only", k<1>}, {"io only", k<2>}, {"io 16B st", k<3>}, {"loads only", k<4>}, {"product", k<5>}, {"prod no st", k<6>}, {"prod no ld", k<7>}};
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
