@@ -119,12 +119,15 @@ def test_cfg3_full(brb, orc, torch_dev, golden):
 
 
 @pytest.mark.parametrize("n,rec_len,off", [
-    (65600, 1500, 0),        # > 1024 groups of 64: line-aligned staging (digest_line.h)
+    (65600, 1500, 0),        # line-aligned staging (digest_line.h), groups handed out by tickets
     (65600, 1500, 4),        # record bases 4 mod 16: every per-lane window shift changes
-    (65601, 1532, 8),        # t = 60: two padding blocks; partial last group
+    (65601, 1532, 8),        # t = 60: two padding blocks; partial last group (per-DMA issue)
     (66000, 1508, 12),       # t = 36
-    (65700, 132, 4),         # 3 lines per record, K = 2
-    (65600, 1504, 0),        # even dword stride: record-relative staging (digest_dma.h)
+    (65700, 132, 4),         # 3 lines per record, K = 2; < 160 B: per-DMA issue on every group
+    (65600, 1504, 0),        # even dword stride
+    (5000, 160, 4),          # smallest length with four DMAs per M0 write (instruction offsets)
+    (5000, 156, 8),          # largest length without
+    (3000, 1501, 0),         # not 4-byte multiple: record-relative stages (digest_dma.h), tickets
 ])
 def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
     data = workload.gen_records(0x5EED0006, 0, n, rec_len)
