@@ -105,13 +105,18 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
     uint32_t w[16];
     uint64_t rb = g0 * 64;                                     // compute cursor: first record of group
     uint32_t cs = 0, slot = lds_base;
+    BRB_LINE_PROBE_DECL
+    BRB_LINE_PROBE(0);
     while (pending) {
         if (is_g < n_groups) {
             issue_next();
+            BRB_LINE_PROBE(1);
             brb_dma::wait_vmcnt<SG::NI * (P - 1)>();
         } else {
+            BRB_LINE_PROBE(1);
             brb_dma::wait_vmcnt<0>();
         }
+        BRB_LINE_PROBE(2);
         --pending;
         if (DYN)
             rb = (slot == lds_base ? slot_g0 : slot_g1) * 64;
@@ -177,6 +182,7 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
         if (!DYN)
             rb += wstride * 64;
     }
+    BRB_LINE_PROBE(3);
 }
 
 // Host-side launch.

@@ -35,7 +35,7 @@ __device__ inline uint64_t pr_rt()
         }                                                                               \
     } while (0)
 
-#include "digest_line.h"
+#include "digest_dma.h"
 #include "md5_device.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -87,15 +87,22 @@ int main(int argc, char **argv)
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
     struct V { const char *name; Kern k; };
     struct VG { const char *name; Kern k; int waves; };
+    VG vs64[] = {{"DMA64 static 4x4", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4},
+                 {"DMA64 dyn16", brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
+                 {"DMA64 dyn8", brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
+                 {"DMA64 only", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
     VG vs[] = {{"LINE md5", brb_digest::digest_line_kernel<AlgLit, 4, true>, 4},
               {"LINE md5 nt dyn8", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
               {"LINE md5 nt dyn4", brb_digest::digest_line_kernel<AlgLit, 4, true, true, true>, 4},
               {"LINE md5 nt", brb_digest::digest_line_kernel<AlgLit, 4, true, true>, 4},
               {"LINE dma-only nt", brb_digest::digest_line_kernel<AlgNull, 4, true, true>, 4}};
     int it = 0;
-    for (auto &v : vs) {
-        // 4-wave workgroups: 2 per CU; 8-wave (dyn): one per CU, groups strided over the grid
-        const unsigned grid = v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, 512))
+    const bool small = L <= 64;
+    const int nv = small ? 4 : int(sizeof(vs) / sizeof(vs[0]));
+    for (int vi = 0; vi < nv; vi++) {
+        const VG &v = small ? vs64[vi] : vs[vi];
+        // 4-wave workgroups: 2 per CU (4 for <= 64 B records); bigger (dyn): one per CU
+        const unsigned grid = v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, small ? 1024 : 512))
                                            : unsigned(std::min<uint64_t>(groups, 256));
         const uint64_t waves = std::min<uint64_t>(uint64_t(grid) * v.waves, groups);
         const unsigned bs = 64 * v.waves;

@@ -153,8 +153,12 @@ int main(int argc, char **argv)
     };
     else vs = {
         {"BPS1 P2 (product)", digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4, 1024},
-        {"BPS1 P2 dyn16 1WG/CU", digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16, -256},
+        {"BPS1 P2 dyn4 grid 1024", digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true, false, true>, 4, -1024},
+        {"BPS1 P2 dyn4 grid 768", digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true, false, true>, 4, -768},
+        {"BPS1 P2 dyn8 grid 512", digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8, -512},
+        {"BPS1 P2 dyn8 grid 384", digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8, -384},
         {"BPS1 P2 dyn8 1WG/CU", digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8, -256},
+        {"BPS1 P2 dyn16 1WG/CU", digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16, -256},
         {"read floor 1024x256", read_floor<false>, 4, -1024},
         {"BPS1 P2 4WG/CU", digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4, 1024},
         {"BPS1 P3 4WG/CU (3 fit)", digest_fixed_dma_kernel<AlgLit, 4, 3, 1, true>, 4, 1024},
