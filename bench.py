@@ -547,11 +547,14 @@ def bench_batcher(args, rank, world, log):
     C = args.records_per_gpu or 16384
     steps = 20 if args.steps is None else args.steps
     warm = 20 if args.warmup is None else args.warmup
-    out = subprocess.run([exe, str(C), "1500", str(steps), str(warm)], check=True, capture_output=True,
-                         text=True, timeout=600).stdout
-    r = json.loads(out.strip().splitlines()[-1])
-    if "error" in r:
-        raise SystemExit("batcher_bench: " + r["error"])
+    def run(zc):
+        out = subprocess.run([exe, str(C), "1500", str(steps), str(warm), str(zc)], check=True, capture_output=True,
+                             text=True, timeout=600).stdout
+        r = json.loads(out.strip().splitlines()[-1])
+        if "error" in r:
+            raise SystemExit("batcher_bench: " + r["error"])
+        return r
+    r, z = run(0), run(1)
     t = r["round_ms_median"] / 1e3
     return {"metric": "GiB/s of payload through the receive-loop transform batcher (SURVEY §8 f2, host-inclusive)",
             "value": r["payload_gib_s"], "unit": "GiB/s", "n_gpus": world, "steps": steps,
@@ -562,6 +565,11 @@ def bench_batcher(args, rank, world, log):
                        "op": "tools/batcher_bench.c: BRB_TransformBatcherRead/Write per buffer + Flush per round",
                        "parallelism": "single GPU"},
             "buffers_per_s": r["buffers_per_s"], "round_ms_min": r["round_ms_min"],
+            "submit_ms_median": r["submit_ms_median"],
+            "zero_copy": {"value": z["payload_gib_s"], "unit": "GiB/s", "ms_per_step": z["round_ms_median"],
+                          "submit_ms_median": z["submit_ms_median"],
+                          "op": "BRB_BATCHER_ZERO_COPY: buffers page-locked once (BRB_CryptoGPU_HostRegister), "
+                                "kernels read them and write results over PCIe, no arena copies"},
             "note": "step = one round: per-buffer submit (copy into the pinned arena), H2D, open + frame kernels, "
                     "D2H, one callback per buffer"}
 

@@ -120,6 +120,8 @@ _SIGNATURES = [
     ("BRB_TransformBatcherFlush", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("BRB_TransformBatcherGetState", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(BRB_RC4_State)]),
+    ("BRB_CryptoGPU_HostRegister", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    ("BRB_CryptoGPU_HostUnregister", ctypes.c_int, [ctypes.c_void_p]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
@@ -420,17 +422,49 @@ def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=No
 
 # ---- receive-loop batching ---------------------------------------------------------
 CRYPTO_FUNC_RC4, CRYPTO_FUNC_RC4_MD5 = 1, 2
+BATCHER_ZERO_COPY = 0x100
 OP_READ, OP_WRITE = 0, 1
 TransformDone = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
                                  ctypes.c_int)
 
 
-class TransformBatcher:
-    """BRB_TransformBatcher*: one event-loop round of many connections per GPU call."""
+class HostRegion:
+    """Page-aligned host memory page-locked for the GPU (BRB_CryptoGPU_HostRegister)."""
 
-    def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5):
+    def __init__(self, size: int):
+        import mmap
         self._L = lib()
-        self.h = self._L.BRB_TransformBatcherCreate(max_conns, max_round_bytes, algo)
+        self.size = size
+        self._mm = mmap.mmap(-1, size)
+        self._view = (ctypes.c_char * size).from_buffer(self._mm)
+        self.addr = ctypes.addressof(self._view)
+        _check(self._L.BRB_CryptoGPU_HostRegister(self.addr, size), "BRB_CryptoGPU_HostRegister")
+
+    def close(self):
+        if self._mm is not None:
+            self._L.BRB_CryptoGPU_HostUnregister(self.addr)
+            del self._view
+            self._mm.close()
+            self._mm = None
+
+    def __del__(self):
+        self.close()
+
+
+class TransformBatcher:
+    """BRB_TransformBatcher*: one event-loop round of many connections per GPU call.
+
+    zero_copy=True creates the batcher with BRB_BATCHER_ZERO_COPY: the kernels read each buffer in
+    place from page-locked host memory.  This wrapper plays the part of a receive loop whose socket
+    buffers are page-locked: it keeps one registered region and places each submitted buffer in it
+    (the batcher itself copies nothing)."""
+
+    def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5, zero_copy: bool = False):
+        self._L = lib()
+        self._region = HostRegion(max(max_round_bytes, 1)) if zero_copy else None
+        self._used = 0
+        self.h = self._L.BRB_TransformBatcherCreate(max_conns, max_round_bytes,
+                                                    algo | (BATCHER_ZERO_COPY if zero_copy else 0))
         if not self.h:
             raise RuntimeError("BRB_TransformBatcherCreate: " + self._L.BRB_CryptoGPU_LastError().decode())
 
@@ -438,6 +472,19 @@ class TransformBatcher:
         if self.h:
             self._L.BRB_TransformBatcherDestroy(self.h)
             self.h = None
+        if self._region is not None:
+            self._region.close()
+            self._region = None
+
+    def _place(self, data: bytes):
+        """Zero-copy mode: the buffer's address inside the registered region (None when full)."""
+        n = len(data)
+        if self._used + n > self._region.size:
+            return None
+        a = self._region.addr + self._used
+        ctypes.memmove(a, bytes(data), n)
+        self._used += n
+        return a
 
     def __del__(self):
         self.close()
@@ -446,9 +493,15 @@ class TransformBatcher:
         _check(self._L.BRB_TransformBatcherEnable(self.h, conn, bytes(key), len(key)), "BRB_TransformBatcherEnable")
 
     def read(self, conn: int, data: bytes) -> int:
+        if self._region is not None:
+            a = self._place(data)
+            return 0 if a is None else self._L.BRB_TransformBatcherRead(self.h, conn, a, len(data))
         return self._L.BRB_TransformBatcherRead(self.h, conn, bytes(data), len(data))
 
     def write(self, conn: int, data: bytes, salt: int) -> int:
+        if self._region is not None:
+            a = self._place(data)
+            return 0 if a is None else self._L.BRB_TransformBatcherWrite(self.h, conn, a, len(data), salt)
         return self._L.BRB_TransformBatcherWrite(self.h, conn, bytes(data), len(data), salt)
 
     def flush(self):
@@ -460,6 +513,7 @@ class TransformBatcher:
 
         fn = TransformDone(cb)
         rc = self._L.BRB_TransformBatcherFlush(self.h, fn, None)
+        self._used = 0
         if rc < 0 or (rc == 0 and self._L.BRB_CryptoGPU_LastError()):
             raise RuntimeError("BRB_TransformBatcherFlush: " + self._L.BRB_CryptoGPU_LastError().decode())
         return res

@@ -32,13 +32,15 @@ hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint
 
 // RC4 (rc4_kernels.hip): 264-byte BRB_RC4_State records, updated in place.  Stream i uses
 // states[sidx ? sidx[i] : i] (sidx: a connection table, the transform batcher's indirection).
+// ooffs: output offsets (nullptr = the input offsets, out mirrors in)
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
-                            const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx = nullptr);
+                            const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx = nullptr,
+                            const uint64_t *ooffs = nullptr);
 hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const uint64_t *offs, const uint32_t *lens,
                                const uint64_t *salts, uint8_t *frames, const uint64_t *foffs, uint64_t n,
                                hipStream_t s, const uint32_t *sidx = nullptr);
 hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                               const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s,
-                              const uint32_t *sidx = nullptr);
+                              const uint32_t *sidx = nullptr, const uint64_t *ooffs = nullptr);
 
 }  // namespace brb

@@ -50,7 +50,8 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
                                                           const uint32_t *__restrict__ lens, uint64_t n,
-                                                          const uint32_t *__restrict__ sidx)
+                                                          const uint32_t *__restrict__ sidx,
+                                                          const uint64_t *__restrict__ ooffs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
     brb_io::BlockSrc src;
     Snk snk;
     src.init(in + off, len);
-    snk.init(out + off, len);
+    snk.init(out + (ooffs ? ooffs[s] : off), len);
     const uint64_t nblk = (len + 63) >> 6;
     uint32_t c[16];
     if (nblk)
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
                                                             const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
                                                             uint8_t *__restrict__ valid,
-                                                            const uint32_t *__restrict__ sidx)
+                                                            const uint32_t *__restrict__ sidx,
+                                                            const uint64_t *__restrict__ ooffs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     brb_io::BlockSrc src;
     Snk snk;
     src.init(in + off, F);
-    snk.init(out + off, F);
+    snk.init(out + (ooffs ? ooffs[s] : off), F);
 
     // frame block 0 = chunks 0..15; the header is chunks 0..7 (frame bytes 0..31)
     uint32_t cur[16];
@@ -269,11 +271,12 @@ inline unsigned grid_for(uint64_t n) { return unsigned((n + kWave - 1) / kWave);
 namespace brb {
 
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
-                            const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx)
+                            const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx,
+                            const uint64_t *ooffs)
 {
     if (n == 0)
         return hipSuccess;
-    rc4_crypt_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx);
+    rc4_crypt_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
     return hipGetLastError();
 }
 
@@ -288,11 +291,12 @@ hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const ui
 }
 
 hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
-                              const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s, const uint32_t *sidx)
+                              const uint32_t *lens, uint64_t n, uint8_t *valid, hipStream_t s, const uint32_t *sidx,
+                              const uint64_t *ooffs)
 {
     if (n == 0)
         return hipSuccess;
-    rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx);
+    rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
     return hipGetLastError();
 }
 

@@ -10,10 +10,17 @@
 //
 // Ordering: a connection's buffers in one direction form one RC4 stream, so a round may hold at
 // most one of them per sub-round; the k-th buffer of a connection in a round runs in sub-round k.
+//
+// Zero-copy rounds (BRB_BATCHER_ZERO_COPY): the callers' buffers are page-locked, Read/Write keep a
+// reference instead of copying them into the arena, the kernels read them over PCIe and write the
+// results straight into the page-locked output arena.  The copy mode spent ~60 % of a round in the
+// submit memcpy (4.9 of 8.1 ms for 16 384 connections x 2 buffers, tools/batcher_bench.c).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "api_util.h"
@@ -34,7 +41,7 @@ inline size_t up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct Item {
     uint32_t conn;
     int op;
-    uint64_t in_off;
+    uint64_t in_off;  // copy mode: offset in the input arena; zero-copy: device address of the buffer
     uint32_t in_len;
     uint64_t out_off;
     uint32_t out_len;
@@ -42,12 +49,59 @@ struct Item {
     uint32_t round;   // sub-round
 };
 
+// Page-locked host ranges registered through BRB_CryptoGPU_HostRegister: host base, length, the
+// device address of the base.  Sorted by host base.
+struct HostRange {
+    uintptr_t h;
+    uint64_t len;
+    uintptr_t d;
+};
+std::mutex g_ranges_mu;
+std::vector<HostRange> g_ranges;
+std::atomic<uint64_t> g_ranges_gen{1};          // bumped by every unregister
+thread_local HostRange t_last{0, 0, 0};          // this thread's last hit, valid while gen matches
+thread_local uint64_t t_last_gen = 0;
+
+// Device address of [p, p + len) if it lies in page-locked memory the GPU can read.
+bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    // a receive loop submits buffers from the same few regions: one compare instead of the lock
+    if (t_last_gen == g_ranges_gen.load(std::memory_order_acquire) && a >= t_last.h && a - t_last.h + len <= t_last.len) {
+        *d = t_last.d + (a - t_last.h);
+        return true;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_ranges_mu);
+        auto it = std::upper_bound(g_ranges.begin(), g_ranges.end(), a,
+                                   [](uintptr_t x, const HostRange &r) { return x < r.h; });
+        if (it != g_ranges.begin()) {
+            --it;
+            if (a >= it->h && a - it->h + len <= it->len) {
+                *d = it->d + (a - it->h);
+                t_last = *it;
+                t_last_gen = g_ranges_gen.load(std::memory_order_relaxed);
+                return true;
+            }
+        }
+    }
+    void *dp = nullptr;                      // page-locked by HIP itself (hipHostMalloc)
+    if (hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) == hipSuccess && dp) {
+        *d = reinterpret_cast<uintptr_t>(dp);
+        return true;
+    }
+    (void)hipGetLastError();
+    return false;
+}
+
 }  // namespace
 
 struct BRB_TransformBatcher {
     uint32_t max_conns = 0;
     uint64_t cap = 0;          // input bytes per round
     int algo = 0;
+    bool zc = false;           // zero-copy rounds
+    uintptr_t out_dev = 0, meta_dev = 0;   // device addresses of h_out, h_meta
     int dev = 0;
     hipStream_t stream = nullptr;
     uint8_t *d_states = nullptr;           // [2][max_conns] x 264 B: read states, then write states
@@ -83,6 +137,8 @@ extern "C" {
 BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t max_round_bytes, int algo)
 {
     brb_api::clear_err();
+    const bool zc = (algo & BRB_BATCHER_ZERO_COPY) != 0;
+    algo &= ~BRB_BATCHER_ZERO_COPY;
     if (max_conns == 0 || max_round_bytes == 0 || (algo != BRB_CRYPTO_FUNC_RC4 && algo != BRB_CRYPTO_FUNC_RC4_MD5)) {
         set_err("max_conns and max_round_bytes must be > 0 and algo RC4 (1) or RC4_MD5 (2)");
         return nullptr;
@@ -93,6 +149,7 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     b->max_conns = max_conns;
     b->cap = max_round_bytes;
     b->algo = algo;
+    b->zc = zc;
     b->enabled.assign(max_conns, 0);
     // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
     b->max_items = 4 * uint64_t(max_conns);
@@ -111,6 +168,15 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
         delete b;
         return nullptr;
     }
+    void *od = nullptr, *md = nullptr;
+    if ((e = hipHostGetDevicePointer(&od, b->h_out, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer(&md, b->h_meta, 0)) != hipSuccess) {
+        fail_hip("hipHostGetDevicePointer", e);
+        delete b;
+        return nullptr;
+    }
+    b->out_dev = reinterpret_cast<uintptr_t>(od);
+    b->meta_dev = reinterpret_cast<uintptr_t>(md);
     return b;
 }
 
@@ -154,8 +220,16 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
         return BRB_BATCH_NOT_DONE;
     }
     Item it{conn, op, b->in_used, len, b->out_used, out_len, salt, 0};
-    if (len)
+    if (b->zc) {
+        uintptr_t d = 0;
+        if (len && !host_to_device(data, len, &d)) {
+            set_err("zero-copy batcher: buffer is not in page-locked memory (BRB_CryptoGPU_HostRegister)");
+            return BRB_BATCH_BADARG;
+        }
+        it.in_off = d;
+    } else if (len) {
         memcpy(b->h_in + b->in_used, data, len);
+    }
     b->in_used += len;
     b->out_used += out_len;
     b->items.push_back(it);
@@ -228,7 +302,8 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
                 if (it.round != r || it.op != op)
                     continue;
                 reinterpret_cast<uint32_t *>(b->h_meta + g.o_sidx)[k] = uint32_t(op) * b->max_conns + it.conn;
-                reinterpret_cast<uint64_t *>(b->h_meta + g.o_offs)[k] = it.in_off;
+                // zero-copy: kernels address input buffers as out_dev + (device address - out_dev)
+                reinterpret_cast<uint64_t *>(b->h_meta + g.o_offs)[k] = b->zc ? it.in_off - uint64_t(b->out_dev) : it.in_off;
                 reinterpret_cast<uint32_t *>(b->h_meta + g.o_lens)[k] = it.in_len;
                 reinterpret_cast<uint64_t *>(b->h_meta + g.o_ooffs)[k] = it.out_off;
                 reinterpret_cast<uint64_t *>(b->h_meta + g.o_salts)[k] = it.salt;
@@ -244,9 +319,11 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         return BRB_BATCH_NOT_DONE;
     }
     hipStream_t s = b->stream;
-    if ((e = hipMemcpyAsync(b->d_in, b->h_in, b->in_used, hipMemcpyHostToDevice, s)) != hipSuccess ||
+    if ((!b->zc && (e = hipMemcpyAsync(b->d_in, b->h_in, b->in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemcpyAsync(b->d_meta, b->h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
         return fail_hip("hipMemcpyAsync H2D", e);
+    uint8_t *zbase = reinterpret_cast<uint8_t *>(b->out_dev);   // zero-copy: inputs and outputs
+    uint8_t *zvalid = reinterpret_cast<uint8_t *>(b->meta_dev);
     size_t vpos = o_valid;
     std::vector<size_t> group_valid(groups.size(), 0);
     for (size_t gi = 0; gi < groups.size(); gi++) {
@@ -256,7 +333,18 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         const uint32_t *lens = reinterpret_cast<const uint32_t *>(b->d_meta + g.o_lens);
         const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_ooffs);
         const uint64_t *salts = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_salts);
-        if (b->algo == BRB_CRYPTO_FUNC_RC4) {
+        if (b->zc) {
+            // inputs read in place over PCIe, outputs written into the page-locked output arena
+            if (b->algo == BRB_CRYPTO_FUNC_RC4) {
+                e = brb::launch_rc4_crypt(b->d_states, zbase, zbase, offs, lens, g.count, s, sidx, ooffs);
+            } else if (g.op == BRB_CRYPTO_OP_WRITE) {
+                e = brb::launch_rc4md5_frame(b->d_states, zbase, offs, lens, salts, zbase, ooffs, g.count, s, sidx);
+            } else {
+                group_valid[gi] = vpos;
+                e = brb::launch_rc4md5_open(b->d_states, zbase, zbase, offs, lens, g.count, zvalid + vpos, s, sidx, ooffs);
+                vpos += g.count;
+            }
+        } else if (b->algo == BRB_CRYPTO_FUNC_RC4) {
             // the output arena mirrors the input arena for RC4 (same offsets, same lengths)
             e = brb::launch_rc4_crypt(b->d_states, b->d_in, b->d_out, offs, lens, g.count, s, sidx);
         } else if (g.op == BRB_CRYPTO_OP_WRITE) {
@@ -270,13 +358,18 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
     }
-    if ((e = hipMemcpyAsync(b->h_out, b->d_out, b->out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-        (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
-         (e = hipMemcpyAsync(b->h_in, b->d_in, b->in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
-        (vpos > o_valid &&
-         (e = hipMemcpyAsync(b->h_meta + o_valid, b->d_meta + o_valid, vpos - o_valid, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
-        (e = hipStreamSynchronize(s)) != hipSuccess)
+    if (b->zc) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess)
+            return fail_hip("round completion", e);
+    } else if ((e = hipMemcpyAsync(b->h_out, b->d_out, b->out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+               (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
+                (e = hipMemcpyAsync(b->h_in, b->d_in, b->in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+               (vpos > o_valid &&
+                (e = hipMemcpyAsync(b->h_meta + o_valid, b->d_meta + o_valid, vpos - o_valid, hipMemcpyDeviceToHost, s)) !=
+                    hipSuccess) ||
+               (e = hipStreamSynchronize(s)) != hipSuccess) {
         return fail_hip("round completion", e);
+    }
     // deliver in submission order; the k-th read item of a group has valid flag k of that group
     std::vector<uint32_t> next_in_group(groups.size(), 0);
     for (const Item &it : b->items) {
@@ -284,7 +377,11 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         const uint32_t k = next_in_group[gi]++;
         int valid = 1;
         const uint8_t *out;
-        if (b->algo == BRB_CRYPTO_FUNC_RC4) {
+        if (b->zc) {
+            out = b->h_out + it.out_off;
+            if (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 && it.op == BRB_CRYPTO_OP_READ)
+                valid = b->h_meta[group_valid[gi] + k];
+        } else if (b->algo == BRB_CRYPTO_FUNC_RC4) {
             out = b->h_out + it.in_off;
         } else if (it.op == BRB_CRYPTO_OP_WRITE) {
             out = b->h_out + it.out_off;
@@ -298,6 +395,46 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
     b->items.clear();
     b->in_used = b->out_used = 0;
     return int64_t(n);
+}
+
+int BRB_CryptoGPU_HostRegister(void *p, uint64_t len)
+{
+    brb_api::clear_err();
+    if (!p || !len) {
+        set_err("NULL or empty host range");
+        return BRB_BATCH_BADARG;
+    }
+    if (int ok = brb_api::device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    hipError_t e = hipHostRegister(p, len, hipHostRegisterMapped);
+    if (e != hipSuccess)
+        return fail_hip("hipHostRegister", e);
+    void *dp = nullptr;
+    if ((e = hipHostGetDevicePointer(&dp, p, 0)) != hipSuccess) {
+        (void)hipHostUnregister(p);
+        return fail_hip("hipHostGetDevicePointer", e);
+    }
+    std::lock_guard<std::mutex> lk(g_ranges_mu);
+    const HostRange r{reinterpret_cast<uintptr_t>(p), len, reinterpret_cast<uintptr_t>(dp)};
+    g_ranges.insert(std::upper_bound(g_ranges.begin(), g_ranges.end(), r.h,
+                                     [](uintptr_t x, const HostRange &q) { return x < q.h; }),
+                    r);
+    return BRB_BATCH_OK;
+}
+
+int BRB_CryptoGPU_HostUnregister(void *p)
+{
+    brb_api::clear_err();
+    std::lock_guard<std::mutex> lk(g_ranges_mu);
+    for (auto it = g_ranges.begin(); it != g_ranges.end(); ++it)
+        if (it->h == reinterpret_cast<uintptr_t>(p)) {
+            g_ranges.erase(it);
+            g_ranges_gen.fetch_add(1, std::memory_order_acq_rel);
+            hipError_t e = hipHostUnregister(p);
+            return e == hipSuccess ? BRB_BATCH_OK : fail_hip("hipHostUnregister", e);
+        }
+    set_err("host range was not registered");
+    return BRB_BATCH_BADARG;
 }
 
 int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op, BRB_RC4_State *out)

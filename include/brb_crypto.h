@@ -205,6 +205,12 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
 #define BRB_CRYPTO_FUNC_RC4_MD5   2       /* COMM_CRYPTO_FUNC_RC4_MD5, :167 */
 #define BRB_CRYPTO_OP_READ        0       /* CRYPTO_OPERATION_READ, libbrb_ev_aio.h:101 */
 #define BRB_CRYPTO_OP_WRITE       1       /* CRYPTO_OPERATION_WRITE, :102 */
+/* OR into `algo` at Create: zero-copy rounds.  Read/Write keep a reference to `data` instead of
+ * copying it: the bytes must lie in page-locked memory (BRB_CryptoGPU_HostRegister, or allocated
+ * page-locked by HIP) and stay unchanged until Flush returns.  The kernels read the buffers over
+ * PCIe and write the results into the batcher's page-locked output arena: no staging memcpy on the
+ * CPU, no bulk H2D/D2H copies.  Read/Write return -1 for a buffer outside page-locked memory. */
+#define BRB_BATCHER_ZERO_COPY     0x100
 typedef struct BRB_TransformBatcher BRB_TransformBatcher;
 typedef void (*BRB_TransformDone)(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid);
 /* NULL on failure (reason in BRB_CryptoGPU_LastError).  A round holds at most max_round_bytes of
@@ -262,6 +268,11 @@ int BRB_MemBufferDecrypt(void *buf, unsigned long size, unsigned int seed, unsig
 int BRB_CryptoGPU_Available(void);
 /* Last error of the calling thread ("" if none). */
 const char *BRB_CryptoGPU_LastError(void);
+/* Page-lock [p, p + len) for the GPU (hipHostRegister, mapped) so that zero-copy batchers can read
+ * it: 1 = done, 0 = no device / HIP error (LastError), -1 = bad arguments.  Unregister takes the
+ * same `p`. */
+int BRB_CryptoGPU_HostRegister(void *p, uint64_t len);
+int BRB_CryptoGPU_HostUnregister(void *p);
 /* Library version string. */
 const char *BRB_CryptoGPU_Version(void);
 

@@ -21,12 +21,13 @@ def torch_dev(brb):
     return torch
 
 
+@pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_event_loop_rounds(brb, orc, torch_dev, algo):
+def test_event_loop_rounds(brb, orc, torch_dev, algo, zero_copy):
     rng = np.random.default_rng(algo)
     C = 300
     keys = [rng.integers(0, 256, int(rng.integers(4, 32)), dtype=np.uint8).tobytes() for _ in range(C)]
-    b = brb.TransformBatcher(C, 8 << 20, algo)
+    b = brb.TransformBatcher(C, 8 << 20, algo, zero_copy=zero_copy)
     ours_r = [orc.rc4_init(k) for k in keys]      # oracle model of the batcher's read states
     ours_w = [orc.rc4_init(k) for k in keys]      # ... and write states
     peer_w = [orc.rc4_init(k) for k in keys]      # the peer's write side (produces what we read)
@@ -91,3 +92,29 @@ def test_round_full_and_bad_args(brb, torch_dev):
     assert b.write(0, b"", 0) == 0               # 4 buffers per connection on average
     assert len(b.flush()) == 8
     b.close()
+
+
+def test_zero_copy_needs_page_locked(brb, orc, torch_dev):
+    """Zero-copy rounds refuse a buffer outside page-locked memory and take one inside a region
+    registered with BRB_CryptoGPU_HostRegister (also at an odd offset)."""
+    import ctypes
+    L = brb.lib()
+    h = L.BRB_TransformBatcherCreate(4, 1 << 16, 1 | brb.BATCHER_ZERO_COPY)
+    assert h
+    try:
+        assert L.BRB_TransformBatcherEnable(h, 0, b"key", 3) == 1
+        plain = ctypes.create_string_buffer(b"pageable", 8)
+        assert L.BRB_TransformBatcherRead(h, 0, plain, 8) == -1
+        assert b"page-locked" in L.BRB_CryptoGPU_LastError()
+        reg = brb.crypto.HostRegion(8192)
+        ctypes.memmove(reg.addr + 3, b"in place", 8)
+        assert L.BRB_TransformBatcherRead(h, 0, reg.addr + 3, 8) == 1
+        got = []
+        fn = brb.crypto.TransformDone(lambda _u, c, op, out, n, v: got.append(ctypes.string_at(out, n)))
+        assert L.BRB_TransformBatcherFlush(h, fn, None) == 1
+        assert got == [orc.rc4_crypt(orc.rc4_init(b"key"), b"in place")[1]]
+        assert ctypes.string_at(reg.addr + 3, 8) == b"in place"    # input untouched
+        reg.close()
+        assert L.BRB_CryptoGPU_HostUnregister(ctypes.c_void_p(reg.addr)) == -1
+    finally:
+        L.BRB_TransformBatcherDestroy(h)

@@ -7,7 +7,10 @@
  *
  * Build: gcc -O2 -I include tools/batcher_bench.c -L brb_framework_amd -lbrb_crypto_gpu \
  *            -Wl,-rpath,$PWD/brb_framework_amd -o tools/batcher_bench
- * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3]
+ * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3] [zero_copy=0]
+ *
+ * zero_copy=1: the batcher is created with BRB_BATCHER_ZERO_COPY and the frame / payload buffers
+ * (the loop's socket buffers) are page-locked once with BRB_CryptoGPU_HostRegister.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,8 +52,10 @@ int main(int argc, char **argv)
     const uint32_t C = argc > 1 ? (uint32_t)atoi(argv[1]) : 16384;
     const uint32_t L = argc > 2 ? (uint32_t)atoi(argv[2]) : 1500;
     const int R = argc > 3 ? atoi(argv[3]) : 20, W = argc > 4 ? atoi(argv[4]) : 3;
+    const int zc = argc > 5 ? atoi(argv[5]) : 0;
     const uint32_t F = L + BRB_RC4MD5_HEADER;
-    unsigned char *payload = malloc((size_t)C * L), *frames = malloc((size_t)C * F);
+    const size_t pl_sz = ((size_t)C * L + 4095) & ~(size_t)4095, fr_sz = ((size_t)C * F + 4095) & ~(size_t)4095;
+    unsigned char *payload = aligned_alloc(4096, pl_sz), *frames = aligned_alloc(4096, fr_sz);
     BRB_RC4_State *peer = malloc(sizeof(BRB_RC4_State) * C);
     unsigned char key[16];
     unsigned long long x = 0x5EED00F2ull;
@@ -58,7 +63,13 @@ int main(int argc, char **argv)
         x = x * 6364136223846793005ull + 1442695040888963407ull;
         payload[i] = (unsigned char)(x >> 56);
     }
-    BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) + 4096, BRB_CRYPTO_FUNC_RC4_MD5);
+    if (zc && (BRB_CryptoGPU_HostRegister(payload, pl_sz) != BRB_BATCH_OK ||
+               BRB_CryptoGPU_HostRegister(frames, fr_sz) != BRB_BATCH_OK)) {
+        printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
+        return 1;
+    }
+    BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) + 4096,
+                                                         BRB_CRYPTO_FUNC_RC4_MD5 | (zc ? BRB_BATCHER_ZERO_COPY : 0));
     if (!b) {
         printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
         return 1;
@@ -73,7 +84,7 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    double *t = malloc(sizeof(double) * R);
+    double *t = malloc(sizeof(double) * R), *ts = malloc(sizeof(double) * R);
     Tally tally = {0, 0, 0};
     for (int r = 0; r < W + R; r++) {
         /* the peers' frames for this round (ev_kq_aio_transform.c:212-230 + :281-283) */
@@ -97,8 +108,11 @@ int main(int argc, char **argv)
             BRB_TransformBatcherRead(b, c, frames + (size_t)c * F, F);
             BRB_TransformBatcherWrite(b, c, payload + (size_t)c * L, L, c);
         }
+        const double t1 = now();
         const int64_t n = BRB_TransformBatcherFlush(b, on_done, &round);
         const double dt = now() - t0;
+        if (r >= W)
+            ts[r - W] = t1 - t0;
         if (n != 2 * (int64_t)C || round.valid != round.delivered) {
             printf("{\"error\": \"round %d: %lld delivered, %llu valid: %s\"}\n", r, (long long)n, round.valid,
                    BRB_CryptoGPU_LastError());
@@ -111,10 +125,15 @@ int main(int argc, char **argv)
         }
     }
     qsort(t, R, sizeof(double), cmp_d);
+    qsort(ts, R, sizeof(double), cmp_d);
     const double med = t[R / 2];
-    printf("{\"connections\": %u, \"bytes\": %u, \"rounds\": %d, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
-           "\"payload_gib_s\": %.3f, \"buffers_per_s\": %.0f, \"valid\": %llu, \"delivered\": %llu}\n",
-           C, L, R, med * 1e3, t[0] * 1e3, 2.0 * C * L / med / (1 << 30), 2.0 * C / med, tally.valid, tally.delivered);
+    printf("{\"zero_copy\": %d, \"connections\": %u, \"bytes\": %u, \"rounds\": %d, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
+           "\"submit_ms_median\": %.3f, \"payload_gib_s\": %.3f, \"buffers_per_s\": %.0f, \"valid\": %llu, \"delivered\": %llu}\n",
+           zc, C, L, R, med * 1e3, t[0] * 1e3, ts[R / 2] * 1e3, 2.0 * C * L / med / (1 << 30), 2.0 * C / med, tally.valid, tally.delivered);
     BRB_TransformBatcherDestroy(b);
+    if (zc) {
+        BRB_CryptoGPU_HostUnregister(payload);
+        BRB_CryptoGPU_HostUnregister(frames);
+    }
     return 0;
 }
