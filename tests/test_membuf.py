@@ -99,3 +99,28 @@ def test_membuffer_rejects(brb, torch_dev):
     h = np.zeros(256, np.uint8)
     with pytest.raises((RuntimeError, ValueError)):
         brb.membuf_decrypt(h, 4, 1, offset=8)      # size < offset
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("without_quotes", [False, True])
+def test_kv_file_round_trip(brb, orc, torch_dev, tmp_path, without_quotes):
+    """Encrypted K/V files (key_value.c:464-506): the written bytes are the oracle's
+    MemBufferEncryptData(text, KV_SEED, 0), and reading gives the oracle's MemBufferDecryptData of
+    them (not the text: the reference's keyLen 4/64 asymmetry)."""
+    from brb_framework_amd import kv
+    pairs = [("listen_port", "8080"), ("name", "brb"), (None, "x"), ("path", "/var/lib/brb/" + "d" * 77),
+             ("empty", "")] + [(f"k{i}", str(i * 7919)) for i in range(40)]
+    text = kv.kv_assemble(pairs, without_quotes)
+    assert text.startswith(b"listen_port=8080\n" if without_quotes else b'listen_port="8080"\n')
+    p = tmp_path / "brb.conf"
+    assert kv.kv_write_file(p, pairs, enc=True, without_quotes=without_quotes) == 1
+    buf = bytearray(text) + bytearray(brb.membuf_span(len(text)) + 16)
+    n = orc.membuf_encrypt(buf, len(text), kv.KV_SEED, 0)
+    want = bytes(buf[:n])
+    assert p.read_bytes() == want
+    dbuf = bytearray(want) + bytearray(brb.membuf_span(len(want)) + 16)
+    dn = orc.membuf_decrypt(dbuf, len(want), kv.KV_SEED, 0)
+    assert kv.kv_read_file(p) == bytes(dbuf[:dn])
+    q = tmp_path / "plain.conf"
+    kv.kv_write_file(q, pairs, enc=False, without_quotes=without_quotes)
+    assert kv.kv_read_file(q, enc=False) == text
