@@ -109,6 +109,19 @@ inline size_t align_up(size_t x, size_t a)
     return (x + a - 1) / a * a;
 }
 
+// One-lane-per-item kernels (variable-length digests, RC4 streams, segments, base64) launch one
+// work-item per item, and a launch holds fewer than 2^32 work-items per dimension.
+constexpr uint64_t kMaxItems = (uint64_t(1) << 32) - (uint64_t(1) << 16);
+
+bool items_ok(uint64_t n)
+{
+    if (n <= kMaxItems)
+        return true;
+    set_err("%llu items in one call (at most %llu): split the batch", (unsigned long long)n,
+            (unsigned long long)kMaxItems);
+    return false;
+}
+
 int finish(hipStream_t s, unsigned flags)
 {
     if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC))
@@ -133,6 +146,8 @@ int digest_fixed(FixedLauncher launch, size_t dig_len, const void *data, uint32_
         set_err("NULL data or digests");
         return BRB_BATCH_BADARG;
     }
+    if (rec_len == 0 && !items_ok(n_rec))      // empty records go to a one-lane-per-record kernel
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -167,6 +182,8 @@ int digest_var(VarLauncher launch, size_t dig_len, const void *data, const uint6
         set_err("NULL data, offsets, lengths or digests");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n_rec))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -182,6 +199,10 @@ int digest_var(VarLauncher launch, size_t dig_len, const void *data, const uint6
     for (uint64_t i = 0; i < n_rec; i++) {
         if (lengths[i] == 0)
             continue;
+        if (offsets[i] > UINT64_MAX - lengths[i]) {
+            set_err("record %llu: offset + length wraps", (unsigned long long)i);
+            return BRB_BATCH_BADARG;
+        }
         lo = std::min(lo, offsets[i]);
         hi = std::max(hi, offsets[i] + lengths[i]);
     }
@@ -301,8 +322,9 @@ struct Staging {
     }
 };
 
-// [lo, hi) covered by ranges offsets[i] .. + lengths[i] + extra (empty ranges ignored)
-void span_of(const uint64_t *offs, const uint32_t *lens, uint64_t n, uint64_t extra, uint64_t &lo, uint64_t &hi)
+// [lo, hi) covered by ranges offsets[i] .. + lengths[i] + extra (empty ranges ignored); false (and
+// the error set) when a range wraps the address space
+bool span_of(const uint64_t *offs, const uint32_t *lens, uint64_t n, uint64_t extra, uint64_t &lo, uint64_t &hi)
 {
     lo = UINT64_MAX;
     hi = 0;
@@ -310,11 +332,17 @@ void span_of(const uint64_t *offs, const uint32_t *lens, uint64_t n, uint64_t ex
         const uint64_t len = uint64_t(lens[i]) + extra;
         if (!len)
             continue;
+        if (offs[i] > UINT64_MAX - len) {
+            set_err("range %llu: offset %llu + %llu bytes wraps", (unsigned long long)i, (unsigned long long)offs[i],
+                    (unsigned long long)len);
+            return false;
+        }
         lo = std::min(lo, offs[i]);
         hi = std::max(hi, offs[i] + len);
     }
     if (lo == UINT64_MAX)
         lo = hi = 0;
+    return true;
 }
 
 std::vector<uint64_t> rebase(const uint64_t *offs, uint64_t n, uint64_t lo)
@@ -335,6 +363,8 @@ int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint
         set_err("NULL states, in, out, offsets or lengths");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -347,7 +377,8 @@ int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint
         return finish(s, flags);
     }
     uint64_t lo, hi;
-    span_of(offsets, lengths, n, 0, lo, hi);
+    if (!span_of(offsets, lengths, n, 0, lo, hi))
+        return BRB_BATCH_BADARG;
     const std::vector<uint64_t> roff = rebase(offsets, n, lo);
     const size_t span = size_t(hi - lo);
     Staging st;
@@ -379,6 +410,8 @@ int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_
         set_err("NULL states, payload, offsets, lengths, salts, frames or frame_offsets");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -391,8 +424,8 @@ int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_
         return finish(s, flags);
     }
     uint64_t plo, phi, flo, fhi;
-    span_of(offsets, lengths, n, 0, plo, phi);
-    span_of(frame_offsets, lengths, n, BRB_RC4MD5_HEADER, flo, fhi);
+    if (!span_of(offsets, lengths, n, 0, plo, phi) || !span_of(frame_offsets, lengths, n, BRB_RC4MD5_HEADER, flo, fhi))
+        return BRB_BATCH_BADARG;
     const std::vector<uint64_t> poff = rebase(offsets, n, plo), foff = rebase(frame_offsets, n, flo);
     Staging st;
     const size_t i_st = st.add(states, states, sizeof(BRB_RC4_State) * n);
@@ -425,6 +458,8 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
         set_err("NULL states, frames, out, offsets, lengths or valid");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -437,7 +472,8 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
         return finish(s, flags);
     }
     uint64_t lo, hi;
-    span_of(offsets, lengths, n, 0, lo, hi);
+    if (!span_of(offsets, lengths, n, 0, lo, hi))
+        return BRB_BATCH_BADARG;
     const std::vector<uint64_t> roff = rebase(offsets, n, lo);
     const size_t span = size_t(hi - lo);
     Staging st;
@@ -468,6 +504,8 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
         set_err("NULL data, seg_offsets, seg_lengths, rec_first_seg or digests");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n_rec))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -487,7 +525,8 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
             return BRB_BATCH_BADARG;
         }
     uint64_t lo, hi;
-    span_of(soff + k0, slen + k0, nseg, 0, lo, hi);
+    if (!span_of(soff + k0, slen + k0, nseg, 0, lo, hi))
+        return BRB_BATCH_BADARG;
     const std::vector<uint64_t> roff = rebase(soff + k0, nseg, lo);
     std::vector<uint64_t> rfirst(first, first + n_rec + 1);
     for (uint64_t &f : rfirst)
@@ -521,6 +560,8 @@ int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t 
         set_err("NULL data, offsets, lengths, out, out_offsets or out_lengths");
         return BRB_BATCH_BADARG;
     }
+    if (!items_ok(n))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -539,8 +580,8 @@ int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t 
     for (uint64_t i = 0; i < n; i++)
         olen_max[i] = decode ? 3u * (lens[i] / 4) : 4u * ((lens[i] + 2) / 3);
     uint64_t lo, hi, olo, ohi;
-    span_of(offs, lens, n, 0, lo, hi);
-    span_of(ooffs, olen_max.data(), n, 0, olo, ohi);
+    if (!span_of(offs, lens, n, 0, lo, hi) || !span_of(ooffs, olen_max.data(), n, 0, olo, ohi))
+        return BRB_BATCH_BADARG;
     const std::vector<uint64_t> roff = rebase(offs, n, lo), rooff = rebase(ooffs, n, olo);
     Staging st;
     const size_t i_in = st.add(static_cast<const uint8_t *>(in) + lo, nullptr, size_t(hi - lo));

@@ -143,6 +143,10 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
         set_err("max_conns and max_round_bytes must be > 0 and algo RC4 (1) or RC4_MD5 (2)");
         return nullptr;
     }
+    if (uint64_t(max_conns) * 4 > (uint64_t(1) << 32) - (uint64_t(1) << 16)) {
+        set_err("max_conns %u: a round holds up to 4 buffers per connection, at most 2^32 - 2^16", max_conns);
+        return nullptr;
+    }
     if (brb_api::device_ok() != BRB_BATCH_OK)
         return nullptr;
     auto *b = new BRB_TransformBatcher;

@@ -110,3 +110,20 @@ def test_batch_bad_args(brb):
     assert L.BRB_MD5Batch(None, None, None, 3, None, 0, None) == -1
     assert L.BRB_Blowfish_EncryptBatch(None, None, 3, 0, None) == -1
     assert L.BRB_MD5BatchFixed(None, 64, 0, None, 0, None) == 1      # empty batch: nothing to do
+
+
+def test_batch_refuses_oversized_item_counts(brb):
+    """One-lane-per-item kernels take fewer than 2^32 items per call: larger counts are refused
+    (-1, "split the batch") before any device work, so this runs without a GPU."""
+    import ctypes
+    L = brb.lib()
+    b = ctypes.create_string_buffer(64)
+    n = 1 << 33
+    assert L.BRB_RC4_CryptBatch(b, b, b, b, b, n, 0, None) == -1
+    assert b"split the batch" in L.BRB_CryptoGPU_LastError()
+    assert L.BRB_MD5Batch(b, b, b, n, b, 0, None) == -1
+    assert L.BRB_RC4MD5_OpenBatch(b, b, b, b, b, n, b, 0, None) == -1
+    assert L.BRB_Base64EncodeBatch(b, b, b, n, b, b, 0, None) == -1
+    assert L.BRB_MD5BatchFixed(b, 0, n, b, 0, None) == -1
+    assert L.BRB_TransformBatcherCreate(1 << 31, 1 << 20, 1) is None
+    assert b"max_conns" in L.BRB_CryptoGPU_LastError()
