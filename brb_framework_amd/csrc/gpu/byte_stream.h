@@ -194,6 +194,102 @@ struct BlockSrc {
     }
 };
 
+// BlockSrc for a whole wave: the same blocks, loaded cooperatively.  Instruction q of a load moves
+// the blocks of lanes 16q .. 16q+15, four lanes per block (16 bytes each), so one instruction
+// touches 16 memory lines instead of 64; the blocks are handed to their lanes through a 4 KiB LDS
+// exchange per wave.  A per-lane load of 64 scattered 16-byte pieces keeps the texture path busy for
+// ~150 cycles per instruction, and a lone wave per SIMD waits on it: 65 536 RC4 streams x 1536 B,
+// 121 -> 111 us per pass (tools/mb/rc4_parts.hip).
+// init() and fetch() must be called by all 64 lanes of the wave in uniform control flow, the same
+// number of times; a lane with a shorter (or empty) range receives zero blocks past its end.
+struct BlockSrcW {
+    const uint32_t *p;   // dword holding the range's first byte
+    uint32_t sh;         // 8 * (address & 3)
+    uint64_t len, ndw;   // range bytes; dwords holding any of them
+    uint64_t nb;         // block returned by the next fetch()
+    uint32_t prev;       // dword 16 nb of this lane's range
+    uint8_t *xw;         // this wave's exchange rows: row r = lane r's block
+    uint32_t lane;
+    uint64_t qa[4];      // address of dword 1 + 4 (lane & 3) of the range of lane 16q + lane / 4
+    uint64_t qrem[4];    // dwords of that range from there on
+    uint4 v[4];          // in flight: chunk lane & 3 of block nb of lane 16q + lane / 4
+
+    // chunk c of row r sits at 16 ((c + (r >> 2)) & 3): the row-wise reads and the chunk-wise
+    // writes are both free of bank conflicts
+    static BRB_DEV uint32_t xoff(uint32_t r, uint32_t c) { return r * 64 + 16 * ((c + (r >> 2)) & 3); }
+
+    BRB_DEV void issue(uint64_t b)
+    {
+        const uint64_t base = 16 * b;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (base + 4 <= qrem[q]) {
+                v[q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 4 * base));
+            } else {
+                const uint32_t *d = reinterpret_cast<const uint32_t *>(qa[q]) + base;
+                v[q].x = base + 0 < qrem[q] ? ldg(d + 0) : 0u;
+                v[q].y = base + 1 < qrem[q] ? ldg(d + 1) : 0u;
+                v[q].z = base + 2 < qrem[q] ? ldg(d + 2) : 0u;
+                v[q].w = base + 3 < qrem[q] ? ldg(d + 3) : 0u;
+            }
+        }
+    }
+
+    BRB_DEV void init(const uint8_t *a, uint64_t n, uint8_t *exchange)
+    {
+        const uintptr_t ad = reinterpret_cast<uintptr_t>(a);
+        p = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
+        sh = uint32_t(ad & 3) * 8;
+        len = n;
+        ndw = n ? ((ad & 3) + n + 3) / 4 : 0;
+        prev = ndw ? ldg(p) : 0u;
+        nb = 0;
+        xw = exchange;
+        lane = threadIdx.x & 63;
+        const uint64_t pa = reinterpret_cast<uint64_t>(p);
+        const uint32_t c = lane & 3;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int src = 16 * q + int(lane >> 2);
+            const uint64_t a_r = (uint64_t(uint32_t(__shfl(int(pa >> 32), src))) << 32) | uint32_t(__shfl(int(uint32_t(pa)), src));
+            const uint64_t n_r = (uint64_t(uint32_t(__shfl(int(ndw >> 32), src))) << 32) | uint32_t(__shfl(int(uint32_t(ndw)), src));
+            qa[q] = a_r + 4 * (1 + 4 * c);
+            qrem[q] = n_r > 1 + 4 * c ? n_r - 1 - 4 * c : 0;
+        }
+        issue(0);
+    }
+
+    BRB_DEV void fetch(uint32_t (&c)[16])
+    {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *reinterpret_cast<uint4 *>(xw + xoff(16 * q + (lane >> 2), lane & 3)) = v[q];
+        uint32_t L[16];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 t = *reinterpret_cast<const uint4 *>(xw + xoff(lane, k));
+            L[4 * k] = t.x;
+            L[4 * k + 1] = t.y;
+            L[4 * k + 2] = t.z;
+            L[4 * k + 3] = t.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            c[i] = __builtin_amdgcn_alignbit(L[i], i ? L[i - 1] : prev, sh);
+        prev = L[15];
+        const uint64_t pos = 64 * nb;
+        if (pos + 64 > len) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t q = pos + 4 * i;
+                c[i] = q >= len ? 0u : q + 4 <= len ? c[i] : c[i] & ((1u << (8 * uint32_t(len - q))) - 1u);
+            }
+        }
+        ++nb;
+        issue(nb);
+    }
+};
+
 // The 0x80 end marker of MD5 / SHA-1 padding at byte len % 64 of a (zero-filled) tail block.
 BRB_DEV void add_marker(uint32_t (&w)[16], uint64_t len)
 {

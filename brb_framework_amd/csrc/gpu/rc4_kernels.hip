@@ -21,11 +21,26 @@ constexpr int kWave = 64 * int(kWaves);   // threads per workgroup
 
 BRB_DEV uint32_t clamp4(uint64_t left) { return left >= 4 ? 4u : uint32_t(left); }
 
-// Decrypt frame block b (chunks 16b .. 16b + 15 of a frame of F bytes) into pt and the sink.
-BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, uint64_t b, uint32_t (&pt)[16])
+// Wave-uniform maximum (loop bounds of the cooperative block loads).
+BRB_DEV uint32_t wave_max(uint32_t x)
 {
-    uint32_t c[16];
-    src.fetch(c);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = uint32_t(__shfl_xor(int(x), o));
+        x = y > x ? y : x;
+    }
+    return __builtin_amdgcn_readfirstlane(x);
+}
+
+// BlockSrcW exchange per wave.  Only the plain RC4 pass loads cooperatively: 65 536 x 1500 B,
+// 135 -> 124 us.  The frame and open kernels, whose MD5 work per block hides the per-lane loads,
+// measured slower with it (frame 141 -> 150 us, open 139 -> 143 us, rocprofv3, tools/gpu_ab_lib.sh).
+constexpr uint32_t kXchBytes = 4096;
+
+// Decrypt frame block b (chunks 16b .. 16b + 15 of a frame of F bytes, fetched into c) into pt and
+// the sink.
+BRB_DEV void decrypt_block(const uint32_t (&c)[16], Snk &snk, Gen &g, uint64_t F, uint64_t b, uint32_t (&pt)[16])
+{
     const uint64_t pos = 64 * b;
     if (pos + 64 <= F) {
         uint32_t ks[16];
@@ -47,6 +62,13 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
     }
 }
 
+BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, uint64_t b, uint32_t (&pt)[16])
+{
+    uint32_t c[16];
+    src.fetch(c);
+    decrypt_block(c, snk, g, F, b, pt);
+}
+
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
                                                           const uint32_t *__restrict__ lens, uint64_t n,
@@ -54,37 +76,40 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
                                                           const uint64_t *__restrict__ ooffs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
-    if (s >= n)
-        return;
+    const bool live = s < n;                     // lanes past n only help with the block loads
     Gen g;
     g.P.lds = slot;
     g.P.lw = (threadIdx.x & 63) * 4 + (threadIdx.x >> 6);
-    uint8_t *state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;   // sidx: connection table
-    g.load(state);
-    const uint64_t off = offs[s], len = lens[s];
-    brb_io::BlockSrc src;
+    uint8_t *state = nullptr;
+    uint64_t off = 0, len = 0, ooff = 0;
+    if (live) {
+        state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;   // sidx: connection table
+        g.load(state);
+        off = offs[s];
+        len = lens[s];
+        ooff = ooffs ? ooffs[s] : off;
+    }
+    brb_io::BlockSrcW src;
     Snk snk;
-    src.init(in + off, len);
-    snk.init(out + (ooffs ? ooffs[s] : off), len);
+    src.init(in + off, len, xch + (threadIdx.x >> 6) * kXchBytes);
+    snk.init(out + ooff, len);
     const uint64_t nblk = (len + 63) >> 6;
+    const uint32_t nloop = wave_max(uint32_t(nblk));
     uint32_t c[16];
-    if (nblk)
+    if (nloop)
         src.fetch(c);
-    for (uint64_t b = 0; b < nblk; b++) {
-        const uint64_t pos = 64 * b;
-        if (pos + 64 <= len) {
-            uint32_t ks[16];
+    for (uint32_t b = 0; b < nloop; b++) {
+        const uint64_t pos = 64ull * b;
+        const bool full = pos + 64 <= len;
+        uint32_t ks[16];
+        if (full) {
             g.words(ks);
 #pragma unroll
             for (int i = 0; i < 16; i++)
                 ks[i] ^= c[i];
-            // the next block is taken (and the one after it requested) before this block's stores
-            // go out, so the wait for it never includes them
-            if (b + 1 < nblk)
-                src.fetch(c);
-            snk.put16(ks);
-        } else {
+        } else if (pos < len) {
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 const uint64_t q = pos + 4 * i;
@@ -92,9 +117,17 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
                     snk.put(c[i] ^ g.next_n(clamp4(len - q)));
             }
         }
+        // the next block is taken (and the one after it requested) before this block's stores go
+        // out, so the wait for it never includes them
+        if (b + 1 < nloop)
+            src.fetch(c);
+        if (full)
+            snk.put16(ks);
     }
-    snk.flush();
-    g.store(state);
+    if (live) {
+        snk.flush();
+        g.store(state);
+    }
 }
 
 __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict__ states, const uint8_t *__restrict__ payload,
