@@ -12,9 +12,11 @@
 
 constexpr int ITERS = 256;
 
-template <int KIND>
+template <int KIND, bool HALF = false>
 __global__ void chain(unsigned *out, unsigned long long *cyc, unsigned seed)
 {
+    if (HALF && (threadIdx.x & 63) >= 32)        // EXEC = the low 32 lanes of every wave
+        return;
     unsigned a = seed + threadIdx.x, b = seed * 3 + 1, c = seed ^ 0x55, d = threadIdx.x * 7, e = 9, f = 11, g = 13, h = 17;
     const unsigned s = seed | 1;
     unsigned long long t0 = clock64();
@@ -55,20 +57,20 @@ __global__ void chain(unsigned *out, unsigned long long *cyc, unsigned seed)
         cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int K>
+template <int K, bool HALF = false>
 int run(const char *name, int instrs_per_rep, int blocks, int threads)
 {
     unsigned *o;
     unsigned long long *c;
     CK(hipMalloc(&o, blocks * threads * 4));
     CK(hipMalloc(&c, blocks * 8));
-    hipLaunchKernelGGL(chain<K>, dim3(blocks), dim3(threads), 0, 0, o, c, 1u);
+    hipLaunchKernelGGL((chain<K, HALF>), dim3(blocks), dim3(threads), 0, 0, o, c, 1u);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    hipLaunchKernelGGL(chain<K>, dim3(blocks), dim3(threads), 0, 0, o, c, 2u);
+    hipLaunchKernelGGL((chain<K, HALF>), dim3(blocks), dim3(threads), 0, 0, o, c, 2u);
     hipEventRecord(e1);
     CK(hipDeviceSynchronize());
     float ms;
@@ -101,5 +103,11 @@ int main()
     run<0>("dep v_add_u32, 2 waves/SIMD", 1, 256, 512);
     run<6>("md5-like step, 2 waves/SIMD", 5, 256, 512);
     run<6>("md5-like step, 4 waves/SIMD", 5, 256, 1024);
+    // half-filled waves (32 active lanes): does a wave64 op with half EXEC cost less?
+    run<6, true>("md5-like step, 1 wave/SIMD, 32 lanes", 5, 256, 256);
+    run<6, true>("md5-like step, 2 waves/SIMD, 32 lanes", 5, 256, 512);
+    run<0, true>("dep v_add_u32, 2 waves/SIMD, 32 lanes", 1, 256, 512);
+    run<7, true>("8 chains v_add_u32, 32 lanes", 8, 256, 256);
+    run<7>("8 chains v_add_u32, 64 lanes", 8, 256, 256);
     return 0;
 }
