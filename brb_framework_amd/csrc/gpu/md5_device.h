@@ -10,7 +10,7 @@
 
 #define BRB_MD5_F1(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
 #define BRB_MD5_F2(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
-#define BRB_MD5_F3(x, y, z) ((x) ^ (y) ^ (z))
+#define BRB_MD5_F3(x, y, z) __builtin_amdgcn_bitop3_b32((x), (y), (z), 0x96)   // x ^ y ^ z
 #define BRB_MD5_F4(x, y, z) ((y) ^ ((x) | ~(z)))
 #define BRB_MD5_STEP(F, a, b, c, d, m, k, s) (a) = (b) + rotl<s>((a) + F((b), (c), (d)) + ((m) + (k)))
 
@@ -284,11 +284,13 @@ BRB_DEV void md5_finish(Md5State &st, uint32_t (&w)[16], uint32_t t, uint64_t to
 
 // The padding block of a message whose length is a multiple of 64 (md5.c:134-168 with t = 0):
 // 0x80, zeros, the bit length.  Compile-time words except the length (wave-uniform), so m + K folds
-// into constants and each step is 4 VALU instead of 5.
+// into constants and each step is 4 VALU instead of 5.  Round 3 takes the plain form here
+// (bitop3 xor3 -> add3 with the folded constant): with no message add to hide, v_xad would cost
+// the c ^ d op on top.
 BRB_DEV void md5_pad_only(Md5State &st, uint64_t total_len)
 {
     uint32_t w[16] = {0x80u};
     w[14] = uint32_t(total_len << 3);
     w[15] = uint32_t(total_len >> 29);
-    md5_compress(st, w);
+    md5_compress<false>(st, w);
 }
