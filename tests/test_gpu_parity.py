@@ -232,3 +232,36 @@ def test_c_caller_batch_on_gpu(brb, tmp_path):
     assert res["batch_md5_rc"] == "1"
     assert res["batch_md5_eq"] == "1" and res["batch_sha1_eq"] == "1" and res["batch_bf_eq"] == "1"
     assert res["batch_rc4_eq"] == "1"
+
+
+def test_concurrent_host_threads(brb, orc, torch_dev):
+    """§8(b) threading: the batch API is called from several event-loop threads at once (ctypes
+    drops the GIL for the call).  Each thread has its own host-mode workspace and error string; the
+    digests of every thread's batches must stay bit-exact, and a bad call in one thread must not
+    leak its error into another."""
+    import threading
+    results, errors = {}, []
+
+    def worker(t):
+        try:
+            for it in range(6):
+                L = [1500, 64, 77, 1501][(t + it) % 4]
+                n = 300 + 37 * t + it
+                data = workload.gen_records(0x7A00 + t, it * 1000, n, L)
+                if t == 3 and it == 2:
+                    assert brb.lib().BRB_MD5BatchFixed(None, 64, 3, None, 0, None) == -1
+                md5 = brb.md5_batch_fixed(data, L, n)
+                sha = brb.sha1_batch_fixed(data, L, n)
+                results[(t, it)] = (np.array_equal(md5, orc.md5_batch_fixed(data, L, n)),
+                                    np.array_equal(sha, orc.sha1_batch_fixed(data, L, n)))
+                assert brb.lib().BRB_CryptoGPU_LastError() == b""
+        except Exception as e:          # surfaced in the main thread below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=100)
+    assert not errors, errors
+    assert len(results) == 24 and all(a and b for a, b in results.values())
