@@ -151,6 +151,20 @@ def test_cfg5_shard_property(brb, torch_dev):
         assert got[i].tobytes() == hashlib.md5(data[i * L:(i + 1) * L].tobytes()).digest()
 
 
+@pytest.mark.parametrize("rec_len", [1500, 1501])
+def test_many_groups_per_wave(brb, orc, torch_dev, rec_len):
+    """Batches large enough that every wave takes several 64-record groups from its workgroup's
+    ticket counter (300 000 records = 4 688 groups over 2 048 wave slots): the line-staged kernel
+    (1500 B) and the record-relative one (1501 B), every digest against the oracle."""
+    n = 300_000
+    data = workload.gen_records(0x5EED0005, 0, n, rec_len)
+    d = to_dev(torch_dev, data)
+    assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(),
+                          orc.md5_batch_fixed(data, rec_len, n, threads=16))
+    assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),
+                          orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+
+
 # ---- Blowfish --------------------------------------------------------------------------------
 @pytest.mark.parametrize("key", [b"TESTKEY", b"brb_framework_k4", bytes(range(56)), b"\xff" * 3])
 @pytest.mark.parametrize("n_blocks", [1, 255, 256, 257, 10007])
