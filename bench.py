@@ -501,7 +501,8 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                    "op": name + " (device mode)", "records_per_gpu": n, "record_bytes": L,
                    "parallelism": f"connection-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(moved / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic(args.pmc_summary, f"f1_{args.op}"),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
                      "note": "algorithmic bytes read+written per step; the bound in practice is the per-byte "
                              "RC4 dependency chain through LDS (DESIGN.md)"},

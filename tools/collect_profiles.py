@@ -71,8 +71,15 @@ def main():
                 with open(os.path.join(prof, f"{tag}_{name}_timed_region.json"), "w") as fo:
                     json.dump(tr, fo, indent=1)
                     fo.write("\n")
-    traffic = {}
-    for sub, key, pat in (("pmc2", "cfg2_md5", "Md5Alg"), ("pmc2s", "cfg2_sha1", "Sha1Alg"), ("pmc4", "cfg4_blowfish", "bf_rep_kernel")):
+    try:                                   # entries of passes this run did not repeat stay
+        traffic = json.load(open(os.path.join(prof, "pmc_traffic.json")))
+    except (OSError, ValueError):
+        traffic = {}
+    # (pass directory, key, kernel filter, dispatches per bench step)
+    for sub, key, pat, per in (("pmc2", "cfg2_md5", "Md5Alg", 1), ("pmc2s", "cfg2_sha1", "Sha1Alg", 1),
+                               ("pmc4", "cfg4_blowfish", "bf_rep_kernel", 1),
+                               ("pmc_rc4", "f1_rc4", "rc4_crypt_kernel", 1),
+                               ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2)):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):
             continue
@@ -83,12 +90,13 @@ def main():
             f.write(summ)
         m = pmc_means(d, pat)
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
-            fetch = m["FETCH_SIZE"] * 2 * 1024
-            write = m["WRITE_SIZE"] * 1024
+            fetch = m["FETCH_SIZE"] * 2 * 1024 * per
+            write = m["WRITE_SIZE"] * 1024 * per
             traffic[key] = int(fetch + write)
             traffic[key + "_detail"] = {"fetch_bytes": int(fetch), "write_bytes": int(write),
                                         "source": f"profiles/{tag}_pmc_{key}.txt",
-                                        "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024 per dispatch"}
+                                        "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024 per dispatch"
+                                                   + (f" x {per} dispatches per step" if per > 1 else "")}
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
         f.write("\n")
