@@ -11,6 +11,7 @@
 #include "digest_dma.h"
 #include "digest_line.h"
 #include "md5_device.h"
+#include "md5_sched.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
