@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "rc4_device.h"
@@ -69,6 +70,8 @@ struct BlockSrc2 {
 // for the row-wise and the chunk-wise access.
 BRB_DEV uint32_t xoff(uint32_t r, uint32_t c) { return r * 64 + 16 * ((c + (r >> 2)) & 3); }
 
+__constant__ uint32_t g_stride;   // bytes between stream starts (>= L; 1540 = 4-byte aligned, not 64)
+
 template <int MODE>   // 9 coop loads, 10 coop loads + coop stores; 8 product loop with two blocks in flight; 0 full, 1 gen only, 2 io only, 3 io only with 16-byte stores, 4 loads only
 // 5 product loop (put16, next block taken before the stores), 6 product loop without stores, 7 product loop without loads
 __global__ __launch_bounds__(256) void k(uint8_t *states, const uint8_t *in, uint8_t *out, uint32_t L, uint64_t n, uint32_t *sink)
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(256) void k(uint8_t *states, const uint8_t *in, uin
     uint8_t *state = states + s * kStateBytes;
     if (MODE != 2)
         g.load(state);
-    const uint64_t off = s * L;
+    const uint64_t off = s * g_stride;
     brb_io::BlockSrc src;
     brb_io::Snk snk;
     if (MODE != 1) {
@@ -244,15 +247,18 @@ __global__ __launch_bounds__(256) void k(uint8_t *states, const uint8_t *in, uin
         sink[0] = acc;
 }
 
-int main()
+int main(int argc, char **argv)
 {
     const uint64_t n = 65536;
     const uint32_t L = 1536;   // whole 64-byte blocks
+    const uint32_t S = argc > 1 ? uint32_t(atoi(argv[1])) : L;
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stride), &S, 4));
+    printf("stride %u\n", S);
     uint8_t *st, *in, *out;
     uint32_t *sink;
     CK(hipMalloc(&st, n * kStateBytes));
-    CK(hipMalloc(&in, n * L));
-    CK(hipMalloc(&out, n * L));
+    CK(hipMalloc(&in, n * S + 64));
+    CK(hipMalloc(&out, n * S + 64));
     CK(hipMalloc(&sink, 64));
     std::vector<uint8_t> h(n * kStateBytes);
     for (uint64_t i = 0; i < n; i++) {
@@ -261,7 +267,7 @@ int main()
     }
     CK(hipMemcpy(st, h.data(), h.size(), hipMemcpyHostToDevice));
     {
-        std::vector<uint8_t> hin(n * L);
+        std::vector<uint8_t> hin(n * S);
         for (size_t i = 0; i < hin.size(); i++) hin[i] = uint8_t(i * 2654435761u >> 13);
         CK(hipMemcpy(in, hin.data(), hin.size(), hipMemcpyHostToDevice));
     }
@@ -283,16 +289,17 @@ int main()
                 printf("%-10s %8.1f us per launch  (%.1f ns per byte per stream)\n", v.name, ms * 100, ms * 1e5 / L);
         }
     // coop variants must write what the product loop writes
-    std::vector<uint8_t> ref(n * L), got(n * L);
+    std::vector<uint8_t> ref(n * S), got(n * S);
     CK(hipMemcpy(st, h.data(), h.size(), hipMemcpyHostToDevice));
+    CK(hipMemset(out, 0, n * S));
     hipLaunchKernelGGL(k<5>, dim3(n / 256), dim3(256), 0, 0, st, in, out, L, n, sink);
-    CK(hipMemcpy(ref.data(), out, n * L, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(ref.data(), out, n * S, hipMemcpyDeviceToHost));
     for (int m = 9; m <= 10; m++) {
         CK(hipMemcpy(st, h.data(), h.size(), hipMemcpyHostToDevice));
-        CK(hipMemset(out, 0, n * L));
+        CK(hipMemset(out, 0, n * S));
         if (m == 9) hipLaunchKernelGGL(k<9>, dim3(n / 256), dim3(256), 0, 0, st, in, out, L, n, sink);
         else hipLaunchKernelGGL(k<10>, dim3(n / 256), dim3(256), 0, 0, st, in, out, L, n, sink);
-        CK(hipMemcpy(got.data(), out, n * L, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(got.data(), out, n * S, hipMemcpyDeviceToHost));
         printf("mode %d output %s\n", m, got == ref ? "matches" : "DIFFERS");
     }
     return 0;
