@@ -29,6 +29,7 @@ from .crypto import (  # noqa: F401
     TransformBatcher,
     HostRegion,
     BATCHER_ZERO_COPY,
+    BATCHER_PIPELINED,
     base64_decode_batch,
     base64_encode_batch,
     blowfish_ctx_bytes,
@@ -63,5 +64,5 @@ __all__ = [
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
     "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "base64_decode_batch",
     "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
-    "HostRegion", "BATCHER_ZERO_COPY",
+    "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED",
 ]

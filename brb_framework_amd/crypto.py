@@ -118,6 +118,7 @@ _SIGNATURES = [
     ("BRB_TransformBatcherWrite", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64]),
     ("BRB_TransformBatcherFlush", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("BRB_TransformBatcherFlushAsync", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("BRB_TransformBatcherGetState", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(BRB_RC4_State)]),
     ("BRB_CryptoGPU_HostRegister", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
@@ -423,6 +424,7 @@ def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=No
 # ---- receive-loop batching ---------------------------------------------------------
 CRYPTO_FUNC_RC4, CRYPTO_FUNC_RC4_MD5 = 1, 2
 BATCHER_ZERO_COPY = 0x100
+BATCHER_PIPELINED = 0x200    # BRB_BATCHER_PIPELINED: two arenas, flush_async()
 OP_READ, OP_WRITE = 0, 1
 TransformDone = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
                                  ctypes.c_int)
@@ -457,14 +459,22 @@ class TransformBatcher:
     zero_copy=True creates the batcher with BRB_BATCHER_ZERO_COPY: the kernels read each buffer in
     place from page-locked host memory.  This wrapper plays the part of a receive loop whose socket
     buffers are page-locked: it keeps one registered region and places each submitted buffer in it
-    (the batcher itself copies nothing)."""
+    (the batcher itself copies nothing).
 
-    def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5, zero_copy: bool = False):
+    pipelined=True creates it with BRB_BATCHER_PIPELINED: flush_async() starts the round and returns
+    the previous round's results; flush() drains both.  In zero-copy mode the wrapper then keeps one
+    region per arena, since a running round's buffers must stay unchanged until delivered."""
+
+    def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5, zero_copy: bool = False,
+                 pipelined: bool = False):
         self._L = lib()
-        self._region = HostRegion(max(max_round_bytes, 1)) if zero_copy else None
+        n_reg = 2 if pipelined else 1
+        self._regions = [HostRegion(max(max_round_bytes, 1)) for _ in range(n_reg)] if zero_copy else None
+        self._cur = 0
         self._used = 0
         self.h = self._L.BRB_TransformBatcherCreate(max_conns, max_round_bytes,
-                                                    algo | (BATCHER_ZERO_COPY if zero_copy else 0))
+                                                    algo | (BATCHER_ZERO_COPY if zero_copy else 0) |
+                                                    (BATCHER_PIPELINED if pipelined else 0))
         if not self.h:
             raise RuntimeError("BRB_TransformBatcherCreate: " + self._L.BRB_CryptoGPU_LastError().decode())
 
@@ -472,16 +482,18 @@ class TransformBatcher:
         if self.h:
             self._L.BRB_TransformBatcherDestroy(self.h)
             self.h = None
-        if self._region is not None:
-            self._region.close()
-            self._region = None
+        if self._regions is not None:
+            for r in self._regions:
+                r.close()
+            self._regions = None
 
     def _place(self, data: bytes):
         """Zero-copy mode: the buffer's address inside the registered region (None when full)."""
         n = len(data)
-        if self._used + n > self._region.size:
+        region = self._regions[self._cur]
+        if self._used + n > region.size:
             return None
-        a = self._region.addr + self._used
+        a = region.addr + self._used
         ctypes.memmove(a, bytes(data), n)
         self._used += n
         return a
@@ -493,30 +505,40 @@ class TransformBatcher:
         _check(self._L.BRB_TransformBatcherEnable(self.h, conn, bytes(key), len(key)), "BRB_TransformBatcherEnable")
 
     def read(self, conn: int, data: bytes) -> int:
-        if self._region is not None:
+        if self._regions is not None:
             a = self._place(data)
             return 0 if a is None else self._L.BRB_TransformBatcherRead(self.h, conn, a, len(data))
         return self._L.BRB_TransformBatcherRead(self.h, conn, bytes(data), len(data))
 
     def write(self, conn: int, data: bytes, salt: int) -> int:
-        if self._region is not None:
+        if self._regions is not None:
             a = self._place(data)
             return 0 if a is None else self._L.BRB_TransformBatcherWrite(self.h, conn, a, len(data), salt)
         return self._L.BRB_TransformBatcherWrite(self.h, conn, bytes(data), len(data), salt)
 
-    def flush(self):
-        """Returns [(conn, op, out bytes, valid)] in submission order."""
+    def _run(self, fn_name):
         res = []
 
         def cb(_user, conn, op, out, n, valid):
             res.append((conn, op, ctypes.string_at(out, n) if n else b"", valid))
 
         fn = TransformDone(cb)
-        rc = self._L.BRB_TransformBatcherFlush(self.h, fn, None)
-        self._used = 0
+        launched = self._used > 0
+        rc = getattr(self._L, fn_name)(self.h, fn, None)
         if rc < 0 or (rc == 0 and self._L.BRB_CryptoGPU_LastError()):
-            raise RuntimeError("BRB_TransformBatcherFlush: " + self._L.BRB_CryptoGPU_LastError().decode())
+            raise RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
+        if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
+            self._cur ^= 1      # the running round keeps its region until delivered
+        self._used = 0
         return res
+
+    def flush(self):
+        """Returns [(conn, op, out bytes, valid)] in submission order (every round still pending)."""
+        return self._run("BRB_TransformBatcherFlush")
+
+    def flush_async(self):
+        """Pipelined: starts this round, returns the previous round's [(conn, op, out, valid)]."""
+        return self._run("BRB_TransformBatcherFlushAsync")
 
     def state(self, conn: int, op: int) -> bytes:
         st = BRB_RC4_State()

@@ -94,6 +94,39 @@ bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
     return false;
 }
 
+// One round's arenas and bookkeeping.  A pipelined batcher (BRB_BATCHER_PIPELINED) owns two, so the
+// event loop fills one while the GPU runs the other.
+struct Round {
+    uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr;   // pinned
+    uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr;
+    uintptr_t out_dev = 0, meta_dev = 0;   // device addresses of h_out, h_meta
+    uint64_t in_used = 0, out_used = 0;
+    std::vector<Item> items;
+    // filled by launch_round, read by deliver_round
+    std::vector<int64_t> group_of;         // (sub-round, op) -> group
+    std::vector<size_t> group_valid;       // group -> offset of its valid flags in h_meta
+    hipEvent_t done = nullptr;
+    bool in_flight = false;
+
+    void release()
+    {
+        (void)hipFree(d_in);
+        (void)hipFree(d_out);
+        (void)hipFree(d_meta);
+        (void)hipHostFree(h_in);
+        (void)hipHostFree(h_out);
+        (void)hipHostFree(h_meta);
+        if (done)
+            (void)hipEventDestroy(done);
+    }
+    void reset()
+    {
+        items.clear();
+        in_used = out_used = 0;
+        in_flight = false;
+    }
+};
+
 }  // namespace
 
 struct BRB_TransformBatcher {
@@ -101,16 +134,14 @@ struct BRB_TransformBatcher {
     uint64_t cap = 0;          // input bytes per round
     int algo = 0;
     bool zc = false;           // zero-copy rounds
-    uintptr_t out_dev = 0, meta_dev = 0;   // device addresses of h_out, h_meta
+    int n_rounds = 1;          // 2 when pipelined
+    int cur = 0;               // the round Read/Write fill
     int dev = 0;
     hipStream_t stream = nullptr;
     uint8_t *d_states = nullptr;           // [2][max_conns] x 264 B: read states, then write states
-    uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr;   // pinned
-    uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr;
     size_t out_cap = 0, meta_cap = 0;
     uint64_t max_items = 0;    // buffers per round: 4 per connection on average
-    uint64_t in_used = 0, out_used = 0;
-    std::vector<Item> items;
+    Round r[2];
     std::vector<uint8_t> enabled;
 
     ~BRB_TransformBatcher()
@@ -119,17 +150,31 @@ struct BRB_TransformBatcher {
         if (stream)
             (void)hipStreamSynchronize(stream);
         (void)hipFree(d_states);
-        (void)hipFree(d_in);
-        (void)hipFree(d_out);
-        (void)hipFree(d_meta);
-        (void)hipHostFree(h_in);
-        (void)hipHostFree(h_out);
-        (void)hipHostFree(h_meta);
+        for (Round &x : r)
+            x.release();
         if (stream)
             (void)hipStreamDestroy(stream);
     }
 
     uint8_t *state(uint32_t conn, int op) { return d_states + (size_t(op) * max_conns + conn) * sizeof(BRB_RC4_State); }
+
+    hipError_t alloc_round(Round &x)
+    {
+        hipError_t e;
+        void *od = nullptr, *md = nullptr;
+        if ((e = hipMalloc(&x.d_in, up(cap, kAlign))) != hipSuccess || (e = hipMalloc(&x.d_out, out_cap)) != hipSuccess ||
+            (e = hipMalloc(&x.d_meta, meta_cap)) != hipSuccess ||
+            (e = hipHostMalloc(&x.h_in, up(cap, kAlign), hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc(&x.h_out, out_cap, hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostMalloc(&x.h_meta, meta_cap, hipHostMallocDefault)) != hipSuccess ||
+            (e = hipHostGetDevicePointer(&od, x.h_out, 0)) != hipSuccess ||
+            (e = hipHostGetDevicePointer(&md, x.h_meta, 0)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming)) != hipSuccess)
+            return e;
+        x.out_dev = reinterpret_cast<uintptr_t>(od);
+        x.meta_dev = reinterpret_cast<uintptr_t>(md);
+        return hipSuccess;
+    }
 };
 
 extern "C" {
@@ -138,7 +183,8 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
 {
     brb_api::clear_err();
     const bool zc = (algo & BRB_BATCHER_ZERO_COPY) != 0;
-    algo &= ~BRB_BATCHER_ZERO_COPY;
+    const bool pipelined = (algo & BRB_BATCHER_PIPELINED) != 0;
+    algo &= ~(BRB_BATCHER_ZERO_COPY | BRB_BATCHER_PIPELINED);
     if (max_conns == 0 || max_round_bytes == 0 || (algo != BRB_CRYPTO_FUNC_RC4 && algo != BRB_CRYPTO_FUNC_RC4_MD5)) {
         set_err("max_conns and max_round_bytes must be > 0 and algo RC4 (1) or RC4_MD5 (2)");
         return nullptr;
@@ -154,6 +200,7 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     b->cap = max_round_bytes;
     b->algo = algo;
     b->zc = zc;
+    b->n_rounds = pipelined ? 2 : 1;
     b->enabled.assign(max_conns, 0);
     // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
     b->max_items = 4 * uint64_t(max_conns);
@@ -162,25 +209,17 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     hipError_t e;
     if ((e = hipGetDevice(&b->dev)) != hipSuccess || (e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&b->d_states, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
-        (e = hipMemset(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
-        (e = hipMalloc(&b->d_in, up(max_round_bytes, kAlign))) != hipSuccess ||
-        (e = hipMalloc(&b->d_out, b->out_cap)) != hipSuccess || (e = hipMalloc(&b->d_meta, b->meta_cap)) != hipSuccess ||
-        (e = hipHostMalloc(&b->h_in, up(max_round_bytes, kAlign), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc(&b->h_out, b->out_cap, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc(&b->h_meta, b->meta_cap, hipHostMallocDefault)) != hipSuccess) {
+        (e = hipMemset(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess) {
         fail_hip("transform batcher allocation", e);
         delete b;
         return nullptr;
     }
-    void *od = nullptr, *md = nullptr;
-    if ((e = hipHostGetDevicePointer(&od, b->h_out, 0)) != hipSuccess ||
-        (e = hipHostGetDevicePointer(&md, b->h_meta, 0)) != hipSuccess) {
-        fail_hip("hipHostGetDevicePointer", e);
-        delete b;
-        return nullptr;
-    }
-    b->out_dev = reinterpret_cast<uintptr_t>(od);
-    b->meta_dev = reinterpret_cast<uintptr_t>(md);
+    for (int i = 0; i < b->n_rounds; i++)
+        if ((e = b->alloc_round(b->r[i])) != hipSuccess) {
+            fail_hip("transform batcher round allocation", e);
+            delete b;
+            return nullptr;
+        }
     return b;
 }
 
@@ -216,14 +255,15 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
         set_err("bad batcher, data or connection (not enabled?)");
         return BRB_BATCH_BADARG;
     }
+    Round &R = b->r[b->cur];
     const uint32_t out_len = len + (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 && op == BRB_CRYPTO_OP_WRITE ? kHdr : 0);
-    const size_t meta_need = kMetaItem * (b->items.size() + 1) + 4096;
-    if (b->items.size() >= b->max_items || b->in_used + len > b->cap || b->out_used + out_len > b->out_cap ||
+    const size_t meta_need = kMetaItem * (R.items.size() + 1) + 4096;
+    if (R.items.size() >= b->max_items || R.in_used + len > b->cap || R.out_used + out_len > b->out_cap ||
         meta_need > b->meta_cap) {
         set_err("round is full: flush first");
         return BRB_BATCH_NOT_DONE;
     }
-    Item it{conn, op, b->in_used, len, b->out_used, out_len, salt, 0};
+    Item it{conn, op, R.in_used, len, R.out_used, out_len, salt, 0};
     if (b->zc) {
         uintptr_t d = 0;
         if (len && !host_to_device(data, len, &d)) {
@@ -232,11 +272,11 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
         }
         it.in_off = d;
     } else if (len) {
-        memcpy(b->h_in + b->in_used, data, len);
+        memcpy(R.h_in + R.in_used, data, len);
     }
-    b->in_used += len;
-    b->out_used += out_len;
-    b->items.push_back(it);
+    R.in_used += len;
+    R.out_used += out_len;
+    R.items.push_back(it);
     return BRB_BATCH_OK;
 }
 
@@ -250,23 +290,17 @@ int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void
     return submit(b, conn, BRB_CRYPTO_OP_WRITE, data, len, salt);
 }
 
-int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
+}  // extern "C"
+
+// Enqueues round R on the batcher's stream: metadata, H2D, the kernels, D2H, then R.done.  Nothing
+// waits here; the stream keeps rounds (and so every connection's RC4 stream) in order.
+static int launch_round(BRB_TransformBatcher *b, Round &R)
 {
-    brb_api::clear_err();
-    if (!b) {
-        set_err("NULL batcher");
-        return BRB_BATCH_BADARG;
-    }
-    const size_t n = b->items.size();
-    if (n == 0)
-        return 0;
     hipError_t e;
-    if ((e = hipSetDevice(b->dev)) != hipSuccess)
-        return fail_hip("hipSetDevice", e);
     // sub-round of every item: its rank among the same connection's items in the same direction
     std::vector<uint32_t> seen(size_t(2) * b->max_conns, 0);
     uint32_t rounds = 0;
-    for (Item &it : b->items) {
+    for (Item &it : R.items) {
         it.round = seen[size_t(it.op) * b->max_conns + it.conn]++;
         rounds = std::max(rounds, it.round + 1);
     }
@@ -277,12 +311,12 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         size_t o_sidx, o_offs, o_lens, o_ooffs, o_salts;
     };
     std::vector<Group> groups;
-    std::vector<int64_t> group_of(size_t(rounds) * 2, -1);   // (sub-round, op) -> group
+    R.group_of.assign(size_t(rounds) * 2, -1);
     size_t m = 0;
     for (uint32_t r = 0; r < rounds; r++)
         for (int op = 0; op < 2; op++) {
             uint32_t c = 0;
-            for (const Item &it : b->items)
+            for (const Item &it : R.items)
                 c += it.round == r && it.op == op;
             if (!c)
                 continue;
@@ -302,41 +336,41 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
                 return BRB_BATCH_NOT_DONE;
             }
             uint32_t k = 0;
-            for (const Item &it : b->items) {
+            for (const Item &it : R.items) {
                 if (it.round != r || it.op != op)
                     continue;
-                reinterpret_cast<uint32_t *>(b->h_meta + g.o_sidx)[k] = uint32_t(op) * b->max_conns + it.conn;
+                reinterpret_cast<uint32_t *>(R.h_meta + g.o_sidx)[k] = uint32_t(op) * b->max_conns + it.conn;
                 // zero-copy: kernels address input buffers as out_dev + (device address - out_dev)
-                reinterpret_cast<uint64_t *>(b->h_meta + g.o_offs)[k] = b->zc ? it.in_off - uint64_t(b->out_dev) : it.in_off;
-                reinterpret_cast<uint32_t *>(b->h_meta + g.o_lens)[k] = it.in_len;
-                reinterpret_cast<uint64_t *>(b->h_meta + g.o_ooffs)[k] = it.out_off;
-                reinterpret_cast<uint64_t *>(b->h_meta + g.o_salts)[k] = it.salt;
+                reinterpret_cast<uint64_t *>(R.h_meta + g.o_offs)[k] = b->zc ? it.in_off - uint64_t(R.out_dev) : it.in_off;
+                reinterpret_cast<uint32_t *>(R.h_meta + g.o_lens)[k] = it.in_len;
+                reinterpret_cast<uint64_t *>(R.h_meta + g.o_ooffs)[k] = it.out_off;
+                reinterpret_cast<uint64_t *>(R.h_meta + g.o_salts)[k] = it.salt;
                 ++k;
             }
-            group_of[size_t(r) * 2 + op] = int64_t(groups.size());
+            R.group_of[size_t(r) * 2 + op] = int64_t(groups.size());
             groups.push_back(g);
         }
     // valid flags: one byte per item of each read group, after the metadata
     const size_t o_valid = m;
-    if (o_valid + n > b->meta_cap) {
+    if (o_valid + R.items.size() > b->meta_cap) {
         set_err("metadata overflow");
         return BRB_BATCH_NOT_DONE;
     }
     hipStream_t s = b->stream;
-    if ((!b->zc && (e = hipMemcpyAsync(b->d_in, b->h_in, b->in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
-        (e = hipMemcpyAsync(b->d_meta, b->h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
+    if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, R.in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
+        (e = hipMemcpyAsync(R.d_meta, R.h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
         return fail_hip("hipMemcpyAsync H2D", e);
-    uint8_t *zbase = reinterpret_cast<uint8_t *>(b->out_dev);   // zero-copy: inputs and outputs
-    uint8_t *zvalid = reinterpret_cast<uint8_t *>(b->meta_dev);
+    uint8_t *zbase = reinterpret_cast<uint8_t *>(R.out_dev);   // zero-copy: inputs and outputs
+    uint8_t *zvalid = reinterpret_cast<uint8_t *>(R.meta_dev);
     size_t vpos = o_valid;
-    std::vector<size_t> group_valid(groups.size(), 0);
+    R.group_valid.assign(groups.size(), 0);
     for (size_t gi = 0; gi < groups.size(); gi++) {
         const Group &g = groups[gi];
-        const uint32_t *sidx = reinterpret_cast<const uint32_t *>(b->d_meta + g.o_sidx);
-        const uint64_t *offs = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_offs);
-        const uint32_t *lens = reinterpret_cast<const uint32_t *>(b->d_meta + g.o_lens);
-        const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_ooffs);
-        const uint64_t *salts = reinterpret_cast<const uint64_t *>(b->d_meta + g.o_salts);
+        const uint32_t *sidx = reinterpret_cast<const uint32_t *>(R.d_meta + g.o_sidx);
+        const uint64_t *offs = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_offs);
+        const uint32_t *lens = reinterpret_cast<const uint32_t *>(R.d_meta + g.o_lens);
+        const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_ooffs);
+        const uint64_t *salts = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_salts);
         if (b->zc) {
             // inputs read in place over PCIe, outputs written into the page-locked output arena
             if (b->algo == BRB_CRYPTO_FUNC_RC4) {
@@ -344,62 +378,134 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
             } else if (g.op == BRB_CRYPTO_OP_WRITE) {
                 e = brb::launch_rc4md5_frame(b->d_states, zbase, offs, lens, salts, zbase, ooffs, g.count, s, sidx);
             } else {
-                group_valid[gi] = vpos;
+                R.group_valid[gi] = vpos;
                 e = brb::launch_rc4md5_open(b->d_states, zbase, zbase, offs, lens, g.count, zvalid + vpos, s, sidx, ooffs);
                 vpos += g.count;
             }
         } else if (b->algo == BRB_CRYPTO_FUNC_RC4) {
             // the output arena mirrors the input arena for RC4 (same offsets, same lengths)
-            e = brb::launch_rc4_crypt(b->d_states, b->d_in, b->d_out, offs, lens, g.count, s, sidx);
+            e = brb::launch_rc4_crypt(b->d_states, R.d_in, R.d_out, offs, lens, g.count, s, sidx);
         } else if (g.op == BRB_CRYPTO_OP_WRITE) {
-            e = brb::launch_rc4md5_frame(b->d_states, b->d_in, offs, lens, salts, b->d_out, ooffs, g.count, s, sidx);
+            e = brb::launch_rc4md5_frame(b->d_states, R.d_in, offs, lens, salts, R.d_out, ooffs, g.count, s, sidx);
         } else {
             // decrypt in place in the input arena, then the frames are copied out with it
-            group_valid[gi] = vpos;
-            e = brb::launch_rc4md5_open(b->d_states, b->d_in, b->d_in, offs, lens, g.count, b->d_meta + vpos, s, sidx);
+            R.group_valid[gi] = vpos;
+            e = brb::launch_rc4md5_open(b->d_states, R.d_in, R.d_in, offs, lens, g.count, R.d_meta + vpos, s, sidx);
             vpos += g.count;
         }
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
     }
-    if (b->zc) {
-        if ((e = hipStreamSynchronize(s)) != hipSuccess)
-            return fail_hip("round completion", e);
-    } else if ((e = hipMemcpyAsync(b->h_out, b->d_out, b->out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
-               (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
-                (e = hipMemcpyAsync(b->h_in, b->d_in, b->in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
-               (vpos > o_valid &&
-                (e = hipMemcpyAsync(b->h_meta + o_valid, b->d_meta + o_valid, vpos - o_valid, hipMemcpyDeviceToHost, s)) !=
-                    hipSuccess) ||
-               (e = hipStreamSynchronize(s)) != hipSuccess) {
+    if (!b->zc && ((e = hipMemcpyAsync(R.h_out, R.d_out, R.out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                   (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
+                    (e = hipMemcpyAsync(R.h_in, R.d_in, R.in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+                   (vpos > o_valid && (e = hipMemcpyAsync(R.h_meta + o_valid, R.d_meta + o_valid, vpos - o_valid,
+                                                          hipMemcpyDeviceToHost, s)) != hipSuccess)))
+        return fail_hip("round D2H", e);
+    if ((e = hipEventRecord(R.done, s)) != hipSuccess)
+        return fail_hip("hipEventRecord", e);
+    R.in_flight = true;
+    return BRB_BATCH_OK;
+}
+
+// Waits for round R and hands every result back in submission order; the k-th read item of a
+// group has valid flag k of that group.  Returns the number of buffers delivered, or -1.
+static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user)
+{
+    hipError_t e;
+    if ((e = hipEventSynchronize(R.done)) != hipSuccess) {
+        R.reset();
         return fail_hip("round completion", e);
     }
-    // deliver in submission order; the k-th read item of a group has valid flag k of that group
-    std::vector<uint32_t> next_in_group(groups.size(), 0);
-    for (const Item &it : b->items) {
-        const int64_t gi = group_of[size_t(it.round) * 2 + it.op];
+    std::vector<uint32_t> next_in_group(R.group_valid.size(), 0);
+    for (const Item &it : R.items) {
+        const int64_t gi = R.group_of[size_t(it.round) * 2 + it.op];
         const uint32_t k = next_in_group[gi]++;
         int valid = 1;
         const uint8_t *out;
         if (b->zc) {
-            out = b->h_out + it.out_off;
+            out = R.h_out + it.out_off;
             if (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 && it.op == BRB_CRYPTO_OP_READ)
-                valid = b->h_meta[group_valid[gi] + k];
+                valid = R.h_meta[R.group_valid[gi] + k];
         } else if (b->algo == BRB_CRYPTO_FUNC_RC4) {
-            out = b->h_out + it.in_off;
+            out = R.h_out + it.in_off;
         } else if (it.op == BRB_CRYPTO_OP_WRITE) {
-            out = b->h_out + it.out_off;
+            out = R.h_out + it.out_off;
         } else {
-            out = b->h_in + it.in_off;
-            valid = b->h_meta[group_valid[gi] + k];
+            out = R.h_in + it.in_off;
+            valid = R.h_meta[R.group_valid[gi] + k];
         }
         if (done)
             done(user, it.conn, it.op, out, it.out_len, valid);
     }
-    b->items.clear();
-    b->in_used = b->out_used = 0;
-    return int64_t(n);
+    const int64_t n = int64_t(R.items.size());
+    R.reset();
+    return n;
 }
+
+extern "C" {
+
+int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
+{
+    brb_api::clear_err();
+    if (!b) {
+        set_err("NULL batcher");
+        return BRB_BATCH_BADARG;
+    }
+    hipError_t e;
+    if ((e = hipSetDevice(b->dev)) != hipSuccess)
+        return fail_hip("hipSetDevice", e);
+    int64_t total = 0;
+    Round &prev = b->r[b->cur ^ (b->n_rounds - 1)];
+    if (b->n_rounds == 2 && prev.in_flight) {   // the round FlushAsync left running comes first
+        const int64_t n = deliver_round(b, prev, done, user);
+        if (n < 0)
+            return n;
+        total += n;
+    }
+    Round &R = b->r[b->cur];
+    if (R.items.empty())
+        return total;
+    int rc = launch_round(b, R);
+    if (rc != BRB_BATCH_OK) {
+        if (rc < 0)   // enqueue failed: the round is lost, the stream may hold part of it
+            R.reset();
+        return rc;
+    }
+    const int64_t n = deliver_round(b, R, done, user);
+    return n < 0 ? n : total + n;
+}
+
+int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
+{
+    brb_api::clear_err();
+    if (!b) {
+        set_err("NULL batcher");
+        return BRB_BATCH_BADARG;
+    }
+    if (b->n_rounds == 1)
+        return BRB_TransformBatcherFlush(b, done, user);
+    hipError_t e;
+    if ((e = hipSetDevice(b->dev)) != hipSuccess)
+        return fail_hip("hipSetDevice", e);
+    Round &R = b->r[b->cur], &prev = b->r[b->cur ^ 1];
+    if (!R.items.empty()) {
+        // enqueue this round first so the GPU has it while the previous round's callbacks run
+        int rc = launch_round(b, R);
+        if (rc != BRB_BATCH_OK) {
+            if (rc < 0)
+                R.reset();
+            return rc;
+        }
+    }
+    if (R.in_flight)
+        b->cur ^= 1;   // Read/Write now fill the other arena (the previous round's, once delivered)
+    return prev.in_flight ? deliver_round(b, prev, done, user) : 0;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 int BRB_CryptoGPU_HostRegister(void *p, uint64_t len)
 {

@@ -211,6 +211,9 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
  * PCIe and write the results into the batcher's page-locked output arena: no staging memcpy on the
  * CPU, no bulk H2D/D2H copies.  Read/Write return -1 for a buffer outside page-locked memory. */
 #define BRB_BATCHER_ZERO_COPY     0x100
+/* OR into `algo` at Create: pipelined rounds.  The batcher owns two rounds' arenas, so the loop fills
+ * round k+1 while the GPU runs round k (BRB_TransformBatcherFlushAsync).  Twice the arena memory. */
+#define BRB_BATCHER_PIPELINED     0x200
 typedef struct BRB_TransformBatcher BRB_TransformBatcher;
 typedef void (*BRB_TransformDone)(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid);
 /* NULL on failure (reason in BRB_CryptoGPU_LastError).  A round holds at most max_round_bytes of
@@ -221,8 +224,15 @@ void BRB_TransformBatcherDestroy(BRB_TransformBatcher *b);
 int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const void *key, int key_sz);
 int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
 int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
-/* Runs the round; returns the number of buffers delivered, or -1 / 0 as the batch calls do. */
+/* Runs the round; returns the number of buffers delivered, or -1 / 0 as the batch calls do.  On a
+ * pipelined batcher it first delivers the round FlushAsync left running, so Flush drains everything. */
 int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
+/* Pipelined rounds: enqueues the current round and returns without waiting for it, after delivering
+ * the previous round (if one is running) in submission order; Read/Write then fill the other arena.
+ * Returns the number of buffers delivered (those of the previous round), or -1 / 0 as Flush.  A
+ * connection's streams stay in order across rounds (one HIP stream).  In zero-copy mode a buffer
+ * must stay unchanged until its round is delivered.  Without BRB_BATCHER_PIPELINED this is Flush. */
+int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
 /* Copies a connection's current state (op = READ or WRITE) back to the host (tests, migration). */
 int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op, BRB_RC4_State *out);
 

@@ -21,13 +21,23 @@ def torch_dev(brb):
     return torch
 
 
+def _check_round(got, expect, rnd):
+    assert len(got) == len(expect), rnd
+    for g, e in zip(got, expect):
+        assert g[0] == e[0] and g[1] == e[1] and g[2] == e[2] and g[3] == e[3], (rnd, e[0], e[1])
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_event_loop_rounds(brb, orc, torch_dev, algo, zero_copy):
+def test_event_loop_rounds(brb, orc, torch_dev, algo, zero_copy, pipelined):
+    """pipelined: BRB_BATCHER_PIPELINED, each round started with FlushAsync, whose results come
+    back from the next round's FlushAsync (the last from Flush)."""
     rng = np.random.default_rng(algo)
     C = 300
     keys = [rng.integers(0, 256, int(rng.integers(4, 32)), dtype=np.uint8).tobytes() for _ in range(C)]
-    b = brb.TransformBatcher(C, 8 << 20, algo, zero_copy=zero_copy)
+    b = brb.TransformBatcher(C, 8 << 20, algo, zero_copy=zero_copy, pipelined=pipelined)
+    pending = None
     ours_r = [orc.rc4_init(k) for k in keys]      # oracle model of the batcher's read states
     ours_w = [orc.rc4_init(k) for k in keys]      # ... and write states
     peer_w = [orc.rc4_init(k) for k in keys]      # the peer's write side (produces what we read)
@@ -68,12 +78,20 @@ def test_event_loop_rounds(brb, orc, torch_dev, algo, zero_copy):
                     ours_w[c], wire = orc.rc4_crypt(ours_w[c], payload)
                     expect.append((c, 1, wire, 1))
                 assert b.write(c, payload, salt) == 1
-        got = b.flush()
-        assert len(got) == len(expect)
-        for g, e in zip(got, expect):
-            assert g[0] == e[0] and g[1] == e[1] and g[2] == e[2] and g[3] == e[3], (rnd, e[0], e[1])
-        for c in range(0, C, 7):
+        if pipelined:
+            got = b.flush_async()
+            if pending is None:
+                assert got == []
+            else:
+                _check_round(got, pending, rnd - 1)
+            pending = expect
+        else:
+            _check_round(b.flush(), expect, rnd)
+        for c in range(0, C, 7):     # GetState waits for the stream: the running round is included
             assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
+    if pipelined:
+        _check_round(b.flush(), pending, 5)
+        assert b.flush() == [] and b.flush_async() == []
     b.close()
 
 

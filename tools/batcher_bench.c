@@ -3,14 +3,18 @@
  * as a C event loop would drive it: per round, every connection receives one RC4+MD5 frame written
  * by its peer and sends one payload; each buffer is one BRB_TransformBatcherRead/Write call, then
  * one Flush delivers the results.  The peer side is built with the library's own compat surface
- * (BRB_RC4_Crypt + BRB_MD5*), outside the timed region.  Prints one JSON object.
+ * (BRB_RC4_Crypt + BRB_MD5*), for every round before the timed region.  Prints one JSON object;
+ * payload_gib_s is over the whole timed window (R rounds of submit + flush, drained at both ends).
  *
  * Build: gcc -O2 -I include tools/batcher_bench.c -L brb_framework_amd -lbrb_crypto_gpu \
  *            -Wl,-rpath,$PWD/brb_framework_amd -o tools/batcher_bench
- * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3] [zero_copy=0]
+ * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3] [zero_copy=0] [pipelined=0]
  *
  * zero_copy=1: the batcher is created with BRB_BATCHER_ZERO_COPY and the frame / payload buffers
  * (the loop's socket buffers) are page-locked once with BRB_CryptoGPU_HostRegister.
+ * pipelined=1: BRB_BATCHER_PIPELINED, each round started with FlushAsync: the loop submits round
+ * k+1 while the GPU runs round k (every round has its own frames, so a running round's buffers stay
+ * unchanged, as zero-copy requires).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -53,6 +57,9 @@ int main(int argc, char **argv)
     const uint32_t L = argc > 2 ? (uint32_t)atoi(argv[2]) : 1500;
     const int R = argc > 3 ? atoi(argv[3]) : 20, W = argc > 4 ? atoi(argv[4]) : 3;
     const int zc = argc > 5 ? atoi(argv[5]) : 0;
+    const int pipelined = argc > 6 ? atoi(argv[6]) : 0;
+    /* every round's frames are built before timing (each depends on the peer's RC4 state) */
+    const int NR = W + R;
     const uint32_t F = L + BRB_RC4MD5_HEADER;
     const size_t pl_sz = ((size_t)C * L + 4095) & ~(size_t)4095, fr_sz = ((size_t)C * F + 4095) & ~(size_t)4095;
     unsigned char *payload = aligned_alloc(4096, pl_sz), *frames = aligned_alloc(4096, fr_sz);
@@ -69,7 +76,8 @@ int main(int argc, char **argv)
         return 1;
     }
     BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) + 4096,
-                                                         BRB_CRYPTO_FUNC_RC4_MD5 | (zc ? BRB_BATCHER_ZERO_COPY : 0));
+                                                         BRB_CRYPTO_FUNC_RC4_MD5 | (zc ? BRB_BATCHER_ZERO_COPY : 0) |
+                                                             (pipelined ? BRB_BATCHER_PIPELINED : 0));
     if (!b) {
         printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
         return 1;
@@ -84,12 +92,19 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    double *t = malloc(sizeof(double) * R), *ts = malloc(sizeof(double) * R);
-    Tally tally = {0, 0, 0};
-    for (int r = 0; r < W + R; r++) {
-        /* the peers' frames for this round (ev_kq_aio_transform.c:212-230 + :281-283) */
+    /* the peers' frames for every round, built before timing (ev_kq_aio_transform.c:212-230 +
+     * :281-283): a pipelined round keeps its buffers until the next round delivers it */
+    unsigned char *frames_all = frames;
+    {
+        frames_all = aligned_alloc(4096, fr_sz * NR);
+        if (!frames_all || (zc && BRB_CryptoGPU_HostRegister(frames_all, fr_sz * NR) != BRB_BATCH_OK)) {
+            printf("{\"error\": \"frame arena: %s\"}\n", BRB_CryptoGPU_LastError());
+            return 1;
+        }
+    }
+    for (int r = 0; r < W + R; r++)
         for (uint32_t c = 0; c < C; c++) {
-            unsigned char *f = frames + (size_t)c * F;
+            unsigned char *f = frames_all + (size_t)r * fr_sz + (size_t)c * F;
             BRB_MD5_CTX m;
             BRB_MD5Init(&m);
             BRB_MD5Update(&m, payload + (size_t)c * L, L);
@@ -102,38 +117,58 @@ int main(int argc, char **argv)
             memcpy(f + 30, payload + (size_t)c * L, L);
             BRB_RC4_Crypt(&peer[c], f, f, (int)F);
         }
-        Tally round = {0, 0, 0};
+    double *t = malloc(sizeof(double) * R), *ts = malloc(sizeof(double) * R);
+    Tally tally = {0, 0, 0};
+    double t_start = 0;
+    for (int r = 0; r < W + R; r++) {
+        if (r == W) {   /* drain the warm-up rounds, then time R rounds of submit + flush */
+            if (BRB_TransformBatcherFlush(b, on_done, &tally) < 0) {
+                printf("{\"error\": \"drain: %s\"}\n", BRB_CryptoGPU_LastError());
+                return 1;
+            }
+            t_start = now();
+        }
+        const unsigned char *fr = frames_all + (size_t)r * fr_sz;
         const double t0 = now();
         for (uint32_t c = 0; c < C; c++) {
-            BRB_TransformBatcherRead(b, c, frames + (size_t)c * F, F);
+            BRB_TransformBatcherRead(b, c, fr + (size_t)c * F, F);
             BRB_TransformBatcherWrite(b, c, payload + (size_t)c * L, L, c);
         }
         const double t1 = now();
-        const int64_t n = BRB_TransformBatcherFlush(b, on_done, &round);
-        const double dt = now() - t0;
-        if (r >= W)
+        const int64_t n = pipelined ? BRB_TransformBatcherFlushAsync(b, on_done, &tally)
+                                    : BRB_TransformBatcherFlush(b, on_done, &tally);
+        if (r >= W) {
             ts[r - W] = t1 - t0;
-        if (n != 2 * (int64_t)C || round.valid != round.delivered) {
-            printf("{\"error\": \"round %d: %lld delivered, %llu valid: %s\"}\n", r, (long long)n, round.valid,
-                   BRB_CryptoGPU_LastError());
+            t[r - W] = now() - t0;
+        }
+        if (n < 0 || n != (pipelined && (r == 0 || r == W) ? 0 : 2 * (int64_t)C)) {
+            printf("{\"error\": \"round %d: %lld delivered: %s\"}\n", r, (long long)n, BRB_CryptoGPU_LastError());
             return 1;
         }
-        if (r >= W) {
-            t[r - W] = dt;
-            tally.delivered += round.delivered;
-            tally.valid += round.valid;
-        }
+    }
+    if (BRB_TransformBatcherFlush(b, on_done, &tally) < 0) {
+        printf("{\"error\": \"final flush: %s\"}\n", BRB_CryptoGPU_LastError());
+        return 1;
+    }
+    const double total = now() - t_start, mean = total / R;
+    if (tally.delivered != 2ull * C * (W + R) || tally.valid != tally.delivered) {
+        printf("{\"error\": \"%llu delivered, %llu valid, expected %llu\"}\n", tally.delivered, tally.valid,
+               2ull * C * (W + R));
+        return 1;
     }
     qsort(t, R, sizeof(double), cmp_d);
     qsort(ts, R, sizeof(double), cmp_d);
-    const double med = t[R / 2];
-    printf("{\"zero_copy\": %d, \"connections\": %u, \"bytes\": %u, \"rounds\": %d, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
+    printf("{\"zero_copy\": %d, \"pipelined\": %d, \"connections\": %u, \"bytes\": %u, \"rounds\": %d, "
+           "\"round_ms_mean\": %.3f, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
            "\"submit_ms_median\": %.3f, \"payload_gib_s\": %.3f, \"buffers_per_s\": %.0f, \"valid\": %llu, \"delivered\": %llu}\n",
-           zc, C, L, R, med * 1e3, t[0] * 1e3, ts[R / 2] * 1e3, 2.0 * C * L / med / (1 << 30), 2.0 * C / med, tally.valid, tally.delivered);
+           zc, pipelined, C, L, R, mean * 1e3, t[R / 2] * 1e3, t[0] * 1e3, ts[R / 2] * 1e3,
+           2.0 * C * L / mean / (1 << 30), 2.0 * C / mean, tally.valid, tally.delivered);
     BRB_TransformBatcherDestroy(b);
     if (zc) {
         BRB_CryptoGPU_HostUnregister(payload);
         BRB_CryptoGPU_HostUnregister(frames);
+        if (frames_all != frames)
+            BRB_CryptoGPU_HostUnregister(frames_all);
     }
     return 0;
 }
