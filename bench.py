@@ -543,20 +543,21 @@ def bench_batcher(args, rank, world, log):
     src = exe + ".c"
     lib = os.path.join(ROOT, "brb_framework_amd")
     if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
-        subprocess.run(["gcc", "-O2", "-I", os.path.join(ROOT, "include"), src, "-L", lib, "-lbrb_crypto_gpu",
+        subprocess.run(["gcc", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"), src, "-L", lib, "-lbrb_crypto_gpu",
                         f"-Wl,-rpath,{lib}", "-o", exe], check=True)
     C = args.records_per_gpu or 16384
     steps = 20 if args.steps is None else args.steps
     warm = 20 if args.warmup is None else args.warmup
-    def run(zc, pipelined=0):
-        out = subprocess.run([exe, str(C), "1500", str(steps), str(warm), str(zc), str(pipelined)], check=True,
+    def run(zc, pipelined=0, threads=1):
+        out = subprocess.run([exe, str(C), "1500", str(steps), str(warm), str(zc), str(pipelined), str(threads)],
+                             check=True,
                              capture_output=True,
                              text=True, timeout=600).stdout
         r = json.loads(out.strip().splitlines()[-1])
         if "error" in r:
             raise SystemExit("batcher_bench: " + r["error"])
         return r
-    r, z, rp, zp = run(0), run(1), run(0, 1), run(1, 1)
+    r, z, rp, zp, rp4 = run(0), run(1), run(0, 1), run(1, 1), run(0, 1, 4)
     t = r["round_ms_mean"] / 1e3
     return {"metric": "GiB/s of payload through the receive-loop transform batcher (SURVEY §8 f2, host-inclusive)",
             "value": r["payload_gib_s"], "unit": "GiB/s", "n_gpus": world, "steps": steps,
@@ -576,6 +577,8 @@ def bench_batcher(args, rank, world, log):
                                    "submit_ms_median": rp["submit_ms_median"]},
                           "zero_copy": {"value": zp["payload_gib_s"], "ms_per_step": zp["round_ms_mean"],
                                         "submit_ms_median": zp["submit_ms_median"]},
+                          "copy_4_submit_threads": {"value": rp4["payload_gib_s"], "ms_per_step": rp4["round_ms_mean"],
+                                                    "submit_ms_median": rp4["submit_ms_median"]},
                           "unit": "GiB/s",
                           "op": "BRB_BATCHER_PIPELINED: FlushAsync per round, the loop submits round k+1 while "
                                 "the GPU runs round k"},

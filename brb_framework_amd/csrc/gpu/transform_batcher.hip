@@ -59,18 +59,23 @@ struct HostRange {
 std::mutex g_ranges_mu;
 std::vector<HostRange> g_ranges;
 std::atomic<uint64_t> g_ranges_gen{1};          // bumped by every unregister
-thread_local HostRange t_last{0, 0, 0};          // this thread's last hit, valid while gen matches
+constexpr int kHits = 4;                         // a loop's read pool, write pool, ...
+thread_local HostRange t_last[kHits];            // this thread's last hits, valid while gen matches
+thread_local unsigned t_next = 0;
 thread_local uint64_t t_last_gen = 0;
 
 // Device address of [p, p + len) if it lies in page-locked memory the GPU can read.
 bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    // a receive loop submits buffers from the same few regions: one compare instead of the lock
-    if (t_last_gen == g_ranges_gen.load(std::memory_order_acquire) && a >= t_last.h && a - t_last.h + len <= t_last.len) {
-        *d = t_last.d + (a - t_last.h);
-        return true;
-    }
+    // a receive loop submits buffers from the same few regions (reads and writes alternate between
+    // two pools): a few compares instead of the lock, which several submitting threads would share
+    if (t_last_gen == g_ranges_gen.load(std::memory_order_acquire))
+        for (const HostRange &r : t_last)
+            if (a >= r.h && a - r.h + len <= r.len && r.len) {
+                *d = r.d + (a - r.h);
+                return true;
+            }
     {
         std::lock_guard<std::mutex> lk(g_ranges_mu);
         auto it = std::upper_bound(g_ranges.begin(), g_ranges.end(), a,
@@ -79,8 +84,13 @@ bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
             --it;
             if (a >= it->h && a - it->h + len <= it->len) {
                 *d = it->d + (a - it->h);
-                t_last = *it;
-                t_last_gen = g_ranges_gen.load(std::memory_order_relaxed);
+                const uint64_t gen = g_ranges_gen.load(std::memory_order_relaxed);
+                if (t_last_gen != gen) {
+                    for (HostRange &r : t_last)
+                        r = HostRange{0, 0, 0};
+                    t_last_gen = gen;
+                }
+                t_last[t_next++ % kHits] = *it;
                 return true;
             }
         }
@@ -94,14 +104,52 @@ bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
     return false;
 }
 
+std::atomic<uint64_t> g_round_gen{1};   // round generations, unique across batchers
+
+// Takes up to `want` (at least `need`) units from the shared counter `c` bounded by `cap`; returns
+// the first unit and sets *got, or returns UINT64_MAX when fewer than `need` are left.  The unused
+// tail [ret, ret_end) of the caller's previous chunk is handed back first when nothing was taken
+// after it (always, with one submitting thread), so a lone thread wastes no capacity.
+uint64_t take(std::atomic<uint64_t> &c, uint64_t cap, uint64_t need, uint64_t want, uint64_t *got, uint64_t ret = 0,
+              uint64_t ret_end = 0)
+{
+    if (ret < ret_end) {
+        uint64_t top = ret_end;
+        c.compare_exchange_strong(top, ret, std::memory_order_relaxed);
+    }
+    uint64_t cur = c.load(std::memory_order_relaxed);
+    for (;;) {
+        if (cur > cap || cap - cur < need)
+            return UINT64_MAX;
+        const uint64_t n = std::min(std::max(need, want), cap - cur);
+        if (c.compare_exchange_weak(cur, cur + n, std::memory_order_relaxed)) {
+            *got = n;
+            return cur;
+        }
+    }
+}
+
+// A submitting thread's reserved chunk of one round: slots and arena bytes handed out without
+// touching the shared counters (which bounce between cores when several event threads submit).
+struct Chunk {
+    uint64_t gen = 0;
+    uint64_t slot = 0, slot_end = 0, in = 0, in_end = 0, out = 0, out_end = 0;
+};
+thread_local Chunk t_chunk;
+constexpr uint64_t kChunkSlots = 64, kChunkBytes = 128 << 10;
+
 // One round's arenas and bookkeeping.  A pipelined batcher (BRB_BATCHER_PIPELINED) owns two, so the
 // event loop fills one while the GPU runs the other.
 struct Round {
     uint8_t *h_in = nullptr, *h_out = nullptr, *h_meta = nullptr;   // pinned
     uint8_t *d_in = nullptr, *d_out = nullptr, *d_meta = nullptr;
     uintptr_t out_dev = 0, meta_dev = 0;   // device addresses of h_out, h_meta
-    uint64_t in_used = 0, out_used = 0;
-    std::vector<Item> items;
+    // Read/Write reserve a slot and arena bytes with atomics, so several event threads may submit
+    // into one round at once (their copies run in parallel); a failed reservation leaves a hole.
+    std::vector<Item> slots;               // max_items
+    std::atomic<uint64_t> n_slots{0}, in_used{0}, out_used{0};
+    std::atomic<uint64_t> gen{0};          // new value at every reset: invalidates threads' chunks
+    std::vector<Item> items;               // the launched round's buffers, in slot order
     // filled by launch_round, read by deliver_round
     std::vector<int64_t> group_of;         // (sub-round, op) -> group
     std::vector<size_t> group_valid;       // group -> offset of its valid flags in h_meta
@@ -122,10 +170,16 @@ struct Round {
     void reset()
     {
         items.clear();
-        in_used = out_used = 0;
+        n_slots = 0;
+        in_used = 0;
+        out_used = 0;
         in_flight = false;
+        gen = g_round_gen.fetch_add(1, std::memory_order_relaxed);
     }
+    bool empty() const { return n_slots.load(std::memory_order_relaxed) == 0; }
 };
+
+constexpr uint32_t kHole = 0xFFFFFFFFu;   // Item::conn of a slot whose reservation failed
 
 }  // namespace
 
@@ -173,6 +227,8 @@ struct BRB_TransformBatcher {
             return e;
         x.out_dev = reinterpret_cast<uintptr_t>(od);
         x.meta_dev = reinterpret_cast<uintptr_t>(md);
+        x.slots.resize(max_items);
+        x.gen = g_round_gen.fetch_add(1, std::memory_order_relaxed);
         return hipSuccess;
     }
 };
@@ -257,26 +313,62 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
     }
     Round &R = b->r[b->cur];
     const uint32_t out_len = len + (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 && op == BRB_CRYPTO_OP_WRITE ? kHdr : 0);
-    const size_t meta_need = kMetaItem * (R.items.size() + 1) + 4096;
-    if (R.items.size() >= b->max_items || R.in_used + len > b->cap || R.out_used + out_len > b->out_cap ||
-        meta_need > b->meta_cap) {
-        set_err("round is full: flush first");
-        return BRB_BATCH_NOT_DONE;
+    // Slot order is delivery order.  A thread's slots and bytes come from its own chunks, taken in
+    // increasing order, so the buffers of a connection (owned by one thread) keep their order.
+    // Slots of a chunk left unused stay holes; the metadata arrays fit max_items slots.
+    Chunk &k = t_chunk;
+    const uint64_t gen = R.gen.load(std::memory_order_relaxed);
+    if (k.gen != gen)
+        k = Chunk{gen, 0, 0, 0, 0, 0, 0};
+    uint64_t got;
+    if (k.slot == k.slot_end) {
+        const uint64_t s0 = take(R.n_slots, b->max_items, 1, kChunkSlots, &got);
+        if (s0 == UINT64_MAX) {
+            set_err("round is full: flush first");
+            return BRB_BATCH_NOT_DONE;
+        }
+        for (uint64_t i = s0; i < s0 + got; i++)
+            R.slots[i].conn = kHole;
+        k.slot = s0;
+        k.slot_end = s0 + got;
     }
-    Item it{conn, op, R.in_used, len, R.out_used, out_len, salt, 0};
+    if (k.in_end - k.in < len) {
+        const uint64_t i0 = take(R.in_used, b->cap, len, kChunkBytes, &got, k.in, k.in_end);
+        if (i0 == UINT64_MAX) {
+            k.in = k.in_end = 0;   // the tail may have been handed back: never reuse it
+            set_err("round is full: flush first");
+            return BRB_BATCH_NOT_DONE;
+        }
+        k.in = i0;
+        k.in_end = i0 + got;
+    }
+    if (k.out_end - k.out < out_len) {
+        const uint64_t o0 = take(R.out_used, b->out_cap, out_len, kChunkBytes, &got, k.out, k.out_end);
+        if (o0 == UINT64_MAX) {
+            k.out = k.out_end = 0;
+            set_err("round is full: flush first");
+            return BRB_BATCH_NOT_DONE;
+        }
+        k.out = o0;
+        k.out_end = o0 + got;
+    }
+    Item &it = R.slots[k.slot];
+    const uint64_t in_off = k.in, out_off = k.out;
+    it = Item{conn, op, in_off, len, out_off, out_len, salt, 0};
     if (b->zc) {
         uintptr_t d = 0;
         if (len && !host_to_device(data, len, &d)) {
+            it.conn = kHole;   // this thread's next buffer takes the slot and the bytes
             set_err("zero-copy batcher: buffer is not in page-locked memory (BRB_CryptoGPU_HostRegister)");
             return BRB_BATCH_BADARG;
         }
         it.in_off = d;
     } else if (len) {
-        memcpy(R.h_in + R.in_used, data, len);
+        memcpy(R.h_in + in_off, data, len);
     }
-    R.in_used += len;
-    R.out_used += out_len;
-    R.items.push_back(it);
+    k.slot++;
+    k.in += len;
+    k.out += out_len;
     return BRB_BATCH_OK;
 }
 
@@ -292,11 +384,24 @@ int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void
 
 }  // extern "C"
 
+// The round's buffers in slot order, holes dropped.  Called once no Read/Write is running on R.
+static size_t collect(BRB_TransformBatcher *b, Round &R)
+{
+    const uint64_t n = std::min<uint64_t>(R.n_slots, b->max_items);
+    R.items.clear();
+    for (uint64_t i = 0; i < n; i++)
+        if (R.slots[i].conn != kHole)
+            R.items.push_back(R.slots[i]);
+    return R.items.size();
+}
+
 // Enqueues round R on the batcher's stream: metadata, H2D, the kernels, D2H, then R.done.  Nothing
 // waits here; the stream keeps rounds (and so every connection's RC4 stream) in order.
 static int launch_round(BRB_TransformBatcher *b, Round &R)
 {
     hipError_t e;
+    // arena bytes past the last successful reservation belong to failed ones: not copied
+    const uint64_t in_used = std::min<uint64_t>(R.in_used, b->cap), out_used = std::min<uint64_t>(R.out_used, b->out_cap);
     // sub-round of every item: its rank among the same connection's items in the same direction
     std::vector<uint32_t> seen(size_t(2) * b->max_conns, 0);
     uint32_t rounds = 0;
@@ -357,7 +462,7 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
         return BRB_BATCH_NOT_DONE;
     }
     hipStream_t s = b->stream;
-    if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, R.in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
+    if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (e = hipMemcpyAsync(R.d_meta, R.h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
         return fail_hip("hipMemcpyAsync H2D", e);
     uint8_t *zbase = reinterpret_cast<uint8_t *>(R.out_dev);   // zero-copy: inputs and outputs
@@ -396,9 +501,9 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
     }
-    if (!b->zc && ((e = hipMemcpyAsync(R.h_out, R.d_out, R.out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+    if (!b->zc && ((e = hipMemcpyAsync(R.h_out, R.d_out, out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
                    (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
-                    (e = hipMemcpyAsync(R.h_in, R.d_in, R.in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+                    (e = hipMemcpyAsync(R.h_in, R.d_in, in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
                    (vpos > o_valid && (e = hipMemcpyAsync(R.h_meta + o_valid, R.d_meta + o_valid, vpos - o_valid,
                                                           hipMemcpyDeviceToHost, s)) != hipSuccess)))
         return fail_hip("round D2H", e);
@@ -464,8 +569,10 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         total += n;
     }
     Round &R = b->r[b->cur];
-    if (R.items.empty())
+    if (collect(b, R) == 0) {
+        R.reset();
         return total;
+    }
     int rc = launch_round(b, R);
     if (rc != BRB_BATCH_OK) {
         if (rc < 0)   // enqueue failed: the round is lost, the stream may hold part of it
@@ -489,7 +596,9 @@ int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDon
     if ((e = hipSetDevice(b->dev)) != hipSuccess)
         return fail_hip("hipSetDevice", e);
     Round &R = b->r[b->cur], &prev = b->r[b->cur ^ 1];
-    if (!R.items.empty()) {
+    if (collect(b, R) == 0) {
+        R.reset();
+    } else {
         // enqueue this round first so the GPU has it while the previous round's callbacks run
         int rc = launch_round(b, R);
         if (rc != BRB_BATCH_OK) {

@@ -222,6 +222,10 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
 void BRB_TransformBatcherDestroy(BRB_TransformBatcher *b);
 /* EvAIOReqTransform_CryptoEnable (ev_kq_aio_transform.c:71-105): both states of `conn` = BRB_RC4_Init(key). */
 int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const void *key, int key_sz);
+/* Read/Write may run concurrently on several threads (the reference's mt_engine, ev_kq_base.c:95)
+ * as long as each connection is submitted from one thread; results come back in each connection's
+ * order.  Flush/FlushAsync/Enable must not overlap them.  A thread reserves slots and arena bytes in
+ * chunks, so a round shared by T threads may report full up to T chunks (64 buffers, 128 KiB) early. */
 int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
 int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
 /* Runs the round; returns the number of buffers delivered, or -1 / 0 as the batch calls do.  On a

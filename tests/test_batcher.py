@@ -136,3 +136,58 @@ def test_zero_copy_needs_page_locked(brb, orc, torch_dev):
         assert L.BRB_CryptoGPU_HostUnregister(ctypes.c_void_p(reg.addr)) == -1
     finally:
         L.BRB_TransformBatcherDestroy(h)
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_concurrent_submitters(brb, orc, torch_dev, pipelined):
+    """Several event threads (the reference's mt_engine, ev_kq_base.c:95) submit into one round at
+    once, each owning its connections; every connection's results must come back in its own order
+    and equal the oracle's per-buffer hook.  ctypes releases the GIL, so the Read/Write calls run
+    concurrently."""
+    import threading
+    T, C, rounds = 4, 64, 4
+    rng = np.random.default_rng(7)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(C)]
+    b = brb.TransformBatcher(C, 16 << 20, 2, pipelined=pipelined)
+    for c in range(C):
+        b.enable(c, keys[c])
+    ours_r = [orc.rc4_init(k) for k in keys]
+    ours_w = [orc.rc4_init(k) for k in keys]
+    peer_w = [orc.rc4_init(k) for k in keys]
+    want = {c: [] for c in range(C)}
+    got = {c: [] for c in range(C)}
+    for rnd in range(rounds):
+        work = {t: [] for t in range(T)}          # per thread, in its submission order
+        for c in range(C):
+            for k in range(3):
+                payload = workload.gen_records(0x5EED00F4 + rnd, c * 8 + k, 1, 1 + (c * 37 + k * 101) % 1600).tobytes()
+                if k % 2 == 0:
+                    peer_w[c], frame = orc.rc4md5_frame(peer_w[c], payload, rnd * 100 + c)
+                    ours_r[c], dec, ok = orc.rc4md5_open(ours_r[c], frame)
+                    want[c].append((0, dec, ok))
+                    work[c % T].append(("r", c, frame))
+                else:
+                    ours_w[c], frame = orc.rc4md5_frame(ours_w[c], payload, k)
+                    want[c].append((1, frame, 1))
+                    work[c % T].append(("w", c, payload, k))
+        rcs = []
+
+        def run(t):
+            for item in work[t]:
+                rcs.append(b.read(item[1], item[2]) if item[0] == "r" else b.write(item[1], item[2], item[3]))
+
+        ths = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert rcs == [1] * (3 * C)
+        res = b.flush_async() if pipelined else b.flush()
+        for conn, op, out, valid in res:
+            got[conn].append((op, out, valid))
+    for conn, op, out, valid in b.flush():
+        got[conn].append((op, out, valid))
+    for c in range(C):
+        assert got[c] == want[c], c
+        assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
+    b.close()

@@ -6,16 +6,19 @@
  * (BRB_RC4_Crypt + BRB_MD5*), for every round before the timed region.  Prints one JSON object;
  * payload_gib_s is over the whole timed window (R rounds of submit + flush, drained at both ends).
  *
- * Build: gcc -O2 -I include tools/batcher_bench.c -L brb_framework_amd -lbrb_crypto_gpu \
+ * Build: gcc -O2 -pthread -I include tools/batcher_bench.c -L brb_framework_amd -lbrb_crypto_gpu \
  *            -Wl,-rpath,$PWD/brb_framework_amd -o tools/batcher_bench
- * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3] [zero_copy=0] [pipelined=0]
+ * Run:   tools/batcher_bench [connections=16384] [bytes=1500] [rounds=20] [warmup=3] [zero_copy=0] [pipelined=0] [submit_threads=1]
  *
  * zero_copy=1: the batcher is created with BRB_BATCHER_ZERO_COPY and the frame / payload buffers
  * (the loop's socket buffers) are page-locked once with BRB_CryptoGPU_HostRegister.
  * pipelined=1: BRB_BATCHER_PIPELINED, each round started with FlushAsync: the loop submits round
  * k+1 while the GPU runs round k (every round has its own frames, so a running round's buffers stay
  * unchanged, as zero-copy requires).
+ * submit_threads=T: T threads (the reference's mt_engine) submit disjoint connection ranges into the
+ * same round at once; the main thread is thread 0 and flushes after all T have finished.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -45,6 +48,41 @@ static void on_done(void *user, uint32_t conn, int op, const void *out, uint32_t
     t->bytes += out_len;
 }
 
+/* submit threads: thread t submits connections [t*C/T, (t+1)*C/T) of the current round */
+typedef struct {
+    BRB_TransformBatcher *b;
+    const unsigned char *frames, *payload;
+    uint32_t C, L, F, T;
+    int rounds;                 /* rounds the workers take part in */
+    pthread_barrier_t start, end;
+    int failed;
+} Submit;
+
+static void submit_range(Submit *S, uint32_t t)
+{
+    const uint32_t c0 = (uint32_t)((uint64_t)S->C * t / S->T), c1 = (uint32_t)((uint64_t)S->C * (t + 1) / S->T);
+    for (uint32_t c = c0; c < c1; c++)
+        if (BRB_TransformBatcherRead(S->b, c, S->frames + (size_t)c * S->F, S->F) != BRB_BATCH_OK ||
+            BRB_TransformBatcherWrite(S->b, c, S->payload + (size_t)c * S->L, S->L, c) != BRB_BATCH_OK)
+            __atomic_store_n(&S->failed, 1, __ATOMIC_RELAXED);
+}
+
+typedef struct {
+    Submit *S;
+    uint32_t t;
+} Worker;
+
+static void *worker(void *arg)
+{
+    Worker *w = (Worker *)arg;
+    for (int r = 0; r < w->S->rounds; r++) {
+        pthread_barrier_wait(&w->S->start);
+        submit_range(w->S, w->t);
+        pthread_barrier_wait(&w->S->end);
+    }
+    return NULL;
+}
+
 static int cmp_d(const void *a, const void *b)
 {
     double x = *(const double *)a, y = *(const double *)b;
@@ -58,6 +96,7 @@ int main(int argc, char **argv)
     const int R = argc > 3 ? atoi(argv[3]) : 20, W = argc > 4 ? atoi(argv[4]) : 3;
     const int zc = argc > 5 ? atoi(argv[5]) : 0;
     const int pipelined = argc > 6 ? atoi(argv[6]) : 0;
+    const uint32_t T = argc > 7 && atoi(argv[7]) > 0 ? (uint32_t)atoi(argv[7]) : 1;
     /* every round's frames are built before timing (each depends on the peer's RC4 state) */
     const int NR = W + R;
     const uint32_t F = L + BRB_RC4MD5_HEADER;
@@ -75,7 +114,7 @@ int main(int argc, char **argv)
         printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
         return 1;
     }
-    BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) + 4096,
+    BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) * 102 / 100 + (uint64_t)T * (256 << 10) + 4096,
                                                          BRB_CRYPTO_FUNC_RC4_MD5 | (zc ? BRB_BATCHER_ZERO_COPY : 0) |
                                                              (pipelined ? BRB_BATCHER_PIPELINED : 0));
     if (!b) {
@@ -120,6 +159,24 @@ int main(int argc, char **argv)
     double *t = malloc(sizeof(double) * R), *ts = malloc(sizeof(double) * R);
     Tally tally = {0, 0, 0};
     double t_start = 0;
+    Submit S;
+    memset(&S, 0, sizeof(S));
+    S.b = b;
+    S.payload = payload;
+    S.C = C;
+    S.L = L;
+    S.F = F;
+    S.T = T;
+    S.rounds = W + R;
+    pthread_barrier_init(&S.start, NULL, T);
+    pthread_barrier_init(&S.end, NULL, T);
+    pthread_t *th = malloc(sizeof(pthread_t) * T);
+    Worker *wk = malloc(sizeof(Worker) * T);
+    for (uint32_t i = 1; i < T; i++) {
+        wk[i].S = &S;
+        wk[i].t = i;
+        pthread_create(&th[i], NULL, worker, &wk[i]);
+    }
     for (int r = 0; r < W + R; r++) {
         if (r == W) {   /* drain the warm-up rounds, then time R rounds of submit + flush */
             if (BRB_TransformBatcherFlush(b, on_done, &tally) < 0) {
@@ -130,11 +187,17 @@ int main(int argc, char **argv)
         }
         const unsigned char *fr = frames_all + (size_t)r * fr_sz;
         const double t0 = now();
-        for (uint32_t c = 0; c < C; c++) {
-            BRB_TransformBatcherRead(b, c, fr + (size_t)c * F, F);
-            BRB_TransformBatcherWrite(b, c, payload + (size_t)c * L, L, c);
-        }
+        S.frames = fr;
+        if (T > 1)
+            pthread_barrier_wait(&S.start);
+        submit_range(&S, 0);
+        if (T > 1)
+            pthread_barrier_wait(&S.end);
         const double t1 = now();
+        if (S.failed) {
+            printf("{\"error\": \"round %d: submit failed: %s\"}\n", r, BRB_CryptoGPU_LastError());
+            return 1;
+        }
         const int64_t n = pipelined ? BRB_TransformBatcherFlushAsync(b, on_done, &tally)
                                     : BRB_TransformBatcherFlush(b, on_done, &tally);
         if (r >= W) {
@@ -158,10 +221,12 @@ int main(int argc, char **argv)
     }
     qsort(t, R, sizeof(double), cmp_d);
     qsort(ts, R, sizeof(double), cmp_d);
-    printf("{\"zero_copy\": %d, \"pipelined\": %d, \"connections\": %u, \"bytes\": %u, \"rounds\": %d, "
+    for (uint32_t i = 1; i < T; i++)
+        pthread_join(th[i], NULL);
+    printf("{\"zero_copy\": %d, \"pipelined\": %d, \"submit_threads\": %u, \"connections\": %u, \"bytes\": %u, \"rounds\": %d, "
            "\"round_ms_mean\": %.3f, \"round_ms_median\": %.3f, \"round_ms_min\": %.3f, "
            "\"submit_ms_median\": %.3f, \"payload_gib_s\": %.3f, \"buffers_per_s\": %.0f, \"valid\": %llu, \"delivered\": %llu}\n",
-           zc, pipelined, C, L, R, mean * 1e3, t[R / 2] * 1e3, t[0] * 1e3, ts[R / 2] * 1e3,
+           zc, pipelined, T, C, L, R, mean * 1e3, t[R / 2] * 1e3, t[0] * 1e3, ts[R / 2] * 1e3,
            2.0 * C * L / mean / (1 << 30), 2.0 * C / mean, tally.valid, tally.delivered);
     BRB_TransformBatcherDestroy(b);
     if (zc) {
