@@ -154,6 +154,7 @@ struct Round {
     std::vector<int64_t> group_of;         // (sub-round, op) -> group
     std::vector<size_t> group_valid;       // group -> offset of its valid flags in h_meta
     hipEvent_t done = nullptr;
+    hipEvent_t ev_h2d = nullptr, ev_kern = nullptr;   // pipelined: inputs landed, kernels finished
     bool in_flight = false;
 
     void release()
@@ -164,8 +165,9 @@ struct Round {
         (void)hipHostFree(h_in);
         (void)hipHostFree(h_out);
         (void)hipHostFree(h_meta);
-        if (done)
-            (void)hipEventDestroy(done);
+        for (hipEvent_t ev : {done, ev_h2d, ev_kern})
+            if (ev)
+                (void)hipEventDestroy(ev);
     }
     void reset()
     {
@@ -191,7 +193,10 @@ struct BRB_TransformBatcher {
     int n_rounds = 1;          // 2 when pipelined
     int cur = 0;               // the round Read/Write fill
     int dev = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;          // kernels (and Enable/GetState), in round order
+    // Pipelined: round k+1's H2D and round k's D2H run on their own streams, so the two copy
+    // directions overlap each other and the kernels.  One-round batchers use `stream` for all.
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     uint8_t *d_states = nullptr;           // [2][max_conns] x 264 B: read states, then write states
     size_t out_cap = 0, meta_cap = 0;
     uint64_t max_items = 0;    // buffers per round: 4 per connection on average
@@ -201,13 +206,15 @@ struct BRB_TransformBatcher {
     ~BRB_TransformBatcher()
     {
         (void)hipSetDevice(dev);
-        if (stream)
-            (void)hipStreamSynchronize(stream);
+        for (hipStream_t q : {s_h2d, s_d2h, stream})
+            if (q)
+                (void)hipStreamSynchronize(q);
         (void)hipFree(d_states);
         for (Round &x : r)
             x.release();
-        if (stream)
-            (void)hipStreamDestroy(stream);
+        for (hipStream_t q : {s_h2d, s_d2h, stream})
+            if (q)
+                (void)hipStreamDestroy(q);
     }
 
     uint8_t *state(uint32_t conn, int op) { return d_states + (size_t(op) * max_conns + conn) * sizeof(BRB_RC4_State); }
@@ -223,7 +230,9 @@ struct BRB_TransformBatcher {
             (e = hipHostMalloc(&x.h_meta, meta_cap, hipHostMallocDefault)) != hipSuccess ||
             (e = hipHostGetDevicePointer(&od, x.h_out, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer(&md, x.h_meta, 0)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming)) != hipSuccess)
+            (e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&x.ev_h2d, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&x.ev_kern, hipEventDisableTiming)) != hipSuccess)
             return e;
         x.out_dev = reinterpret_cast<uintptr_t>(od);
         x.meta_dev = reinterpret_cast<uintptr_t>(md);
@@ -267,6 +276,12 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
         (e = hipMalloc(&b->d_states, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
         (e = hipMemset(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess) {
         fail_hip("transform batcher allocation", e);
+        delete b;
+        return nullptr;
+    }
+    if (pipelined && ((e = hipStreamCreateWithFlags(&b->s_h2d, hipStreamNonBlocking)) != hipSuccess ||
+                      (e = hipStreamCreateWithFlags(&b->s_d2h, hipStreamNonBlocking)) != hipSuccess)) {
+        fail_hip("transform batcher copy streams", e);
         delete b;
         return nullptr;
     }
@@ -462,9 +477,14 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
         return BRB_BATCH_NOT_DONE;
     }
     hipStream_t s = b->stream;
-    if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, in_used, hipMemcpyHostToDevice, s)) != hipSuccess) ||
-        (e = hipMemcpyAsync(R.d_meta, R.h_meta, m, hipMemcpyHostToDevice, s)) != hipSuccess)
+    const bool split = b->s_h2d != nullptr;
+    // the arena's previous round was delivered (its done event waited on) before it was refilled
+    hipStream_t sh = split ? b->s_h2d : s;
+    if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, in_used, hipMemcpyHostToDevice, sh)) != hipSuccess) ||
+        (e = hipMemcpyAsync(R.d_meta, R.h_meta, m, hipMemcpyHostToDevice, sh)) != hipSuccess)
         return fail_hip("hipMemcpyAsync H2D", e);
+    if (split && ((e = hipEventRecord(R.ev_h2d, sh)) != hipSuccess || (e = hipStreamWaitEvent(s, R.ev_h2d, 0)) != hipSuccess))
+        return fail_hip("H2D event", e);
     uint8_t *zbase = reinterpret_cast<uint8_t *>(R.out_dev);   // zero-copy: inputs and outputs
     uint8_t *zvalid = reinterpret_cast<uint8_t *>(R.meta_dev);
     size_t vpos = o_valid;
@@ -501,13 +521,16 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
     }
-    if (!b->zc && ((e = hipMemcpyAsync(R.h_out, R.d_out, out_used, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+    hipStream_t sd = split ? b->s_d2h : s;
+    if (split && ((e = hipEventRecord(R.ev_kern, s)) != hipSuccess || (e = hipStreamWaitEvent(sd, R.ev_kern, 0)) != hipSuccess))
+        return fail_hip("kernel event", e);
+    if (!b->zc && ((e = hipMemcpyAsync(R.h_out, R.d_out, out_used, hipMemcpyDeviceToHost, sd)) != hipSuccess ||
                    (b->algo == BRB_CRYPTO_FUNC_RC4_MD5 &&
-                    (e = hipMemcpyAsync(R.h_in, R.d_in, in_used, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
+                    (e = hipMemcpyAsync(R.h_in, R.d_in, in_used, hipMemcpyDeviceToHost, sd)) != hipSuccess) ||
                    (vpos > o_valid && (e = hipMemcpyAsync(R.h_meta + o_valid, R.d_meta + o_valid, vpos - o_valid,
-                                                          hipMemcpyDeviceToHost, s)) != hipSuccess)))
+                                                          hipMemcpyDeviceToHost, sd)) != hipSuccess)))
         return fail_hip("round D2H", e);
-    if ((e = hipEventRecord(R.done, s)) != hipSuccess)
+    if ((e = hipEventRecord(R.done, sd)) != hipSuccess)
         return fail_hip("hipEventRecord", e);
     R.in_flight = true;
     return BRB_BATCH_OK;
