@@ -191,3 +191,31 @@ def test_concurrent_submitters(brb, orc, torch_dev, pipelined):
         assert got[c] == want[c], c
         assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
     b.close()
+
+
+def test_pipelined_edges(brb, orc, torch_dev):
+    """FlushAsync without BRB_BATCHER_PIPELINED is Flush; an empty FlushAsync delivers the running
+    round; a full round still reports 0 and keeps its buffers; Destroy with a round still running
+    waits for it (its results are dropped) instead of freeing memory the GPU is using."""
+    key = b"edge-key"
+    plain = brb.TransformBatcher(1, 4096, 1)
+    plain.enable(0, key)
+    assert plain.read(0, b"abc") == 1
+    assert [r[2] for r in plain.flush_async()] == [orc.rc4_crypt(orc.rc4_init(key), b"abc")[1]]
+    plain.close()
+
+    b = brb.TransformBatcher(1, 1000, 1, pipelined=True)
+    b.enable(0, key)
+    st = orc.rc4_init(key)
+    assert b.read(0, bytes(600)) == 1
+    assert b.read(0, bytes(600)) == 0            # round full: flush first
+    assert b.flush_async() == []                 # round 1 runs
+    assert b.read(0, bytes(600)) == 1            # round 2 fills the other arena
+    got1 = b.flush_async()                       # round 2 runs, round 1 delivered
+    st, want1 = orc.rc4_crypt(st, bytes(600))
+    assert [r[2] for r in got1] == [want1]
+    assert [r[2] for r in b.flush_async()] == [orc.rc4_crypt(st, bytes(600))[1]]   # nothing new
+    assert b.flush() == [] and b.flush_async() == []
+    assert b.read(0, b"left running") == 1
+    assert b.flush_async() == []
+    b.close()                                    # waits for the running round
