@@ -12,6 +12,7 @@ library is missing, ``lib()`` raises; if no GPU is usable, the batch helpers rai
 with the library's own reason.
 """
 from .crypto import (  # noqa: F401
+    BATCH_ALL_DEVICES,
     BATCH_ASYNC,
     BATCH_DEVICE,
     BATCH_HOST,
@@ -36,6 +37,7 @@ from .crypto import (  # noqa: F401
     blowfish_decrypt_batch,
     blowfish_encrypt_batch,
     blowfish_init,
+    device_count,
     exported_symbols,
     gpu_available,
     lib,
@@ -64,5 +66,5 @@ __all__ = [
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
     "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "base64_decode_batch",
     "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
-    "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED",
+    "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED", "BATCH_ALL_DEVICES", "device_count",
 ]

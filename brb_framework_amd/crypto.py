@@ -14,6 +14,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "brb_crypto.h")
 BATCH_HOST = 0x0
 BATCH_DEVICE = 0x1
 BATCH_ASYNC = 0x2
+BATCH_ALL_DEVICES = 0x4
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 ulp = ctypes.POINTER(ctypes.c_ulong)
@@ -124,6 +125,10 @@ _SIGNATURES = [
     ("BRB_CryptoGPU_HostRegister", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("BRB_CryptoGPU_HostUnregister", ctypes.c_int, [ctypes.c_void_p]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
+    ("BRB_CryptoGPU_DeviceCount", ctypes.c_int, []),
+    ("BRB_CryptoGPU_SetDevice", ctypes.c_int, [ctypes.c_int]),
+    ("BRB_CryptoGPU_GetDevice", ctypes.c_int, []),
+    ("BRB_CryptoGPU_ThreadCleanup", None, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
 ]
@@ -185,8 +190,13 @@ def _ptr(x) -> int:
     raise TypeError(f"unsupported buffer type {type(x)}")
 
 
-def _mode(data, stream, async_):
-    """(flags, stream_handle) for a buffer: torch CUDA tensor -> device mode, numpy -> host mode."""
+def _mode(data, stream, async_, all_devices=False):
+    """(flags, stream_handle) for a buffer: torch CUDA tensor -> device mode, numpy -> host mode
+    (all_devices: BRB_BATCH_ALL_DEVICES, host mode only)."""
+    if all_devices:
+        if _is_torch(data):
+            raise ValueError("all_devices needs host (numpy) buffers")
+        return BATCH_HOST | BATCH_ALL_DEVICES, 0
     if _is_torch(data):
         if not data.is_cuda:
             raise ValueError("torch tensors must live on a CUDA (HIP) device; pass numpy for host mode")
@@ -209,40 +219,40 @@ def _nbytes(x) -> int:
     return x.numel() * x.element_size() if _is_torch(x) else x.nbytes
 
 
-def _digest_fixed(fn, width, data, rec_len, n, out, stream, async_):
+def _digest_fixed(fn, width, data, rec_len, n, out, stream, async_, all_devices=False):
     if n is None:
         n = _nbytes(data) // rec_len if rec_len else 0
     if rec_len * n > _nbytes(data):
         raise ValueError("data is smaller than rec_len * n")
     if out is None:
         out = _out_like(data, n, width)
-    flags, h = _mode(data, stream, async_)
+    flags, h = _mode(data, stream, async_, all_devices)
     _check(fn(_ptr(data), rec_len, n, _ptr(out), flags, h), fn.__name__)
     return out
 
 
-def _digest_var(fn, width, data, offsets, lengths, out, stream, async_):
+def _digest_var(fn, width, data, offsets, lengths, out, stream, async_, all_devices=False):
     n = len(offsets)
     if out is None:
         out = _out_like(data, n, width)
-    flags, h = _mode(data, stream, async_)
+    flags, h = _mode(data, stream, async_, all_devices)
     _check(fn(_ptr(data), _ptr(offsets), _ptr(lengths), n, _ptr(out), flags, h), fn.__name__)
     return out
 
 
-def md5_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False):
+def md5_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False, all_devices=False):
     """BRB_MD5BatchFixed: digests (n, 16) of n records of rec_len bytes stored back to back."""
-    return _digest_fixed(lib().BRB_MD5BatchFixed, 16, data, rec_len, n, out, stream, async_)
+    return _digest_fixed(lib().BRB_MD5BatchFixed, 16, data, rec_len, n, out, stream, async_, all_devices)
 
 
-def sha1_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False):
+def sha1_batch_fixed(data, rec_len, n=None, out=None, stream=None, async_=False, all_devices=False):
     """BrbSha1_BatchFixed: digests (n, 20)."""
-    return _digest_fixed(lib().BrbSha1_BatchFixed, 20, data, rec_len, n, out, stream, async_)
+    return _digest_fixed(lib().BrbSha1_BatchFixed, 20, data, rec_len, n, out, stream, async_, all_devices)
 
 
-def md5_batch(data, offsets, lengths, out=None, stream=None, async_=False):
+def md5_batch(data, offsets, lengths, out=None, stream=None, async_=False, all_devices=False):
     """BRB_MD5Batch: offsets uint64[n], lengths uint32[n] (same memory kind as data)."""
-    return _digest_var(lib().BRB_MD5Batch, 16, data, offsets, lengths, out, stream, async_)
+    return _digest_var(lib().BRB_MD5Batch, 16, data, offsets, lengths, out, stream, async_, all_devices)
 
 
 def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, stream=None, async_=False):
@@ -257,8 +267,8 @@ def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, 
     return out
 
 
-def sha1_batch(data, offsets, lengths, out=None, stream=None, async_=False):
-    return _digest_var(lib().BrbSha1_Batch, 20, data, offsets, lengths, out, stream, async_)
+def sha1_batch(data, offsets, lengths, out=None, stream=None, async_=False, all_devices=False):
+    return _digest_var(lib().BrbSha1_Batch, 20, data, offsets, lengths, out, stream, async_, all_devices)
 
 
 # ---- Blowfish ------------------------------------------------------------------------------------
@@ -273,7 +283,7 @@ def blowfish_ctx_bytes(ctx: BRB_BLOWFISH_CTX) -> bytes:
     return ctypes.string_at(ctypes.addressof(ctx), ctypes.sizeof(ctx))
 
 
-def _bf(fn, ctx, words, n_blocks, stream, async_):
+def _bf(fn, ctx, words, n_blocks, stream, async_, all_devices=False):
     """words: uint64 numpy array (host) or int64/uint64 torch CUDA tensor (device), 2 words per block.
     ctx: BRB_BLOWFISH_CTX (host mode) or, in device mode, a CUDA uint8 tensor holding its 8336 bytes
     (a BRB_BLOWFISH_CTX is uploaded for you)."""
@@ -281,7 +291,7 @@ def _bf(fn, ctx, words, n_blocks, stream, async_):
         n_blocks = _nbytes(words) // 16
     if 16 * n_blocks > _nbytes(words):
         raise ValueError("words holds fewer than n_blocks (xl, xr) pairs")
-    flags, h = _mode(words, stream, async_)
+    flags, h = _mode(words, stream, async_, all_devices)
     if flags & BATCH_DEVICE:
         if isinstance(ctx, BRB_BLOWFISH_CTX):
             import torch
@@ -293,12 +303,17 @@ def _bf(fn, ctx, words, n_blocks, stream, async_):
     return words
 
 
-def blowfish_encrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False):
-    return _bf(lib().BRB_Blowfish_EncryptBatch, ctx, words, n_blocks, stream, async_)
+def blowfish_encrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False, all_devices=False):
+    return _bf(lib().BRB_Blowfish_EncryptBatch, ctx, words, n_blocks, stream, async_, all_devices)
 
 
-def blowfish_decrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False):
-    return _bf(lib().BRB_Blowfish_DecryptBatch, ctx, words, n_blocks, stream, async_)
+def blowfish_decrypt_batch(ctx, words, n_blocks=None, stream=None, async_=False, all_devices=False):
+    return _bf(lib().BRB_Blowfish_DecryptBatch, ctx, words, n_blocks, stream, async_, all_devices)
+
+
+def device_count() -> int:
+    """BRB_CryptoGPU_DeviceCount (0 without a usable device)."""
+    return int(lib().BRB_CryptoGPU_DeviceCount())
 
 
 # ---- RC4 and the RC4+MD5 frame (SURVEY §8 f1) ---------------------------------------------------

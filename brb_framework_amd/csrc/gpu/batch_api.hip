@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -17,6 +18,7 @@
 #include "brb_crypto.h"
 #include "api_util.h"
 #include "brb_kernels.h"
+#include "host_pipe.h"
 
 namespace brb_api {
 
@@ -43,17 +45,38 @@ int fail_hip(const char *what, hipError_t e)
     return BRB_BATCH_NOT_DONE;
 }
 
+// The device count is probed once per process: a batch call from the event loop should not pay a
+// runtime query per call, and the set of visible devices does not change while a process runs.
+namespace {
+std::once_flag g_count_once;
+int g_count = 0;
+std::string g_count_err;
+}  // namespace
+
+int device_count()
+{
+    std::call_once(g_count_once, [] {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess) {
+            char buf[256];
+            snprintf(buf, sizeof(buf), "hipGetDeviceCount: %s (%d)", hipGetErrorString(e), int(e));
+            g_count_err = buf;
+            n = 0;
+        } else if (n <= 0) {
+            g_count_err = "no HIP device visible to this process";
+        }
+        g_count = std::max(n, 0);
+    });
+    return g_count;
+}
+
 int device_ok()
 {
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess)
-        return fail_hip("hipGetDeviceCount", e);
-    if (n <= 0) {
-        set_err("no HIP device visible to this process");
-        return BRB_BATCH_NOT_DONE;
-    }
-    return BRB_BATCH_OK;
+    if (device_count() > 0)
+        return BRB_BATCH_OK;
+    t_err = g_count_err;
+    return BRB_BATCH_NOT_DONE;
 }
 
 }  // namespace brb_api
@@ -65,44 +88,66 @@ using brb_api::fail_hip;
 using brb_api::set_err;
 using brb_api::t_err;
 
-// Per-thread, per-device grow-only scratch for host-mode batches.
-struct Workspace {
-    void *ptr = nullptr;
-    size_t cap = 0;
-    int dev = -1;
-};
-thread_local Workspace t_ws;
+}  // namespace
 
+namespace brb_api {
+
+// Per-thread, per-device grow-only scratch for host-mode batches.  Freed when the thread exits
+// (an event thread that ends returns its HBM) or by BRB_CryptoGPU_ThreadCleanup().
+struct Workspaces {
+    std::vector<std::pair<void *, size_t>> by_dev;   // (ptr, capacity) per device ordinal
+    void release()
+    {
+        for (size_t d = 0; d < by_dev.size(); d++)
+            if (by_dev[d].first) {
+                brb_api::DeviceGuard g{int(d)};
+                (void)hipFree(by_dev[d].first);
+                by_dev[d] = {nullptr, 0};
+            }
+    }
+    ~Workspaces() { release(); }
+};
+thread_local Workspaces t_ws;
+
+void release_thread_resources()
+{
+    if (device_count() > 0) {   // host-mode calls have drained their streams before returning
+        t_ws.release();
+        brb_host::release_thread_pipes();
+    }
+}
+
+// Every host-mode call synchronises its stream before it returns (also on its error paths), so a
+// workspace is never freed or regrown while a copy into it is still in flight.
 void *workspace(size_t bytes, hipError_t *err)
 {
     int dev = 0;
     *err = hipGetDevice(&dev);
     if (*err != hipSuccess)
         return nullptr;
-    if (t_ws.ptr && (t_ws.dev != dev || t_ws.cap < bytes)) {
-        if (t_ws.dev == dev) {
-            (void)hipFree(t_ws.ptr);
-        } else {
-            int cur = dev;
-            (void)hipSetDevice(t_ws.dev);
-            (void)hipFree(t_ws.ptr);
-            (void)hipSetDevice(cur);
-        }
-        t_ws.ptr = nullptr;
-        t_ws.cap = 0;
+    if (t_ws.by_dev.size() <= size_t(dev))
+        t_ws.by_dev.resize(dev + 1, {nullptr, 0});
+    auto &w = t_ws.by_dev[dev];
+    if (w.first && w.second < bytes) {
+        (void)hipFree(w.first);
+        w = {nullptr, 0};
     }
-    if (!t_ws.ptr) {
+    if (!w.first) {
         size_t cap = std::max<size_t>(bytes, size_t(1) << 20);
-        *err = hipMalloc(&t_ws.ptr, cap);
-        if (*err != hipSuccess) {
-            t_ws.ptr = nullptr;
+        void *p = nullptr;
+        *err = hipMalloc(&p, cap);
+        if (*err != hipSuccess)
             return nullptr;
-        }
-        t_ws.cap = cap;
-        t_ws.dev = dev;
+        w = {p, cap};
     }
-    return t_ws.ptr;
+    return w.first;
 }
+
+}  // namespace brb_api
+
+namespace {
+
+using brb_api::workspace;
 
 inline size_t align_up(size_t x, size_t a)
 {
@@ -120,6 +165,16 @@ bool items_ok(uint64_t n)
     set_err("%llu items in one call (at most %llu): split the batch", (unsigned long long)n,
             (unsigned long long)kMaxItems);
     return false;
+}
+
+// BRB_BATCH_ALL_DEVICES splits host-mode batches only (device pointers belong to one device).
+bool flags_ok(unsigned flags)
+{
+    if ((flags & BRB_BATCH_ALL_DEVICES) && (flags & BRB_BATCH_DEVICE)) {
+        set_err("BRB_BATCH_ALL_DEVICES needs host pointers (device pointers belong to one device)");
+        return false;
+    }
+    return true;
 }
 
 int finish(hipStream_t s, unsigned flags)
@@ -146,7 +201,7 @@ int digest_fixed(FixedLauncher launch, size_t dig_len, const void *data, uint32_
         set_err("NULL data or digests");
         return BRB_BATCH_BADARG;
     }
-    if (rec_len == 0 && !items_ok(n_rec))      // empty records go to a one-lane-per-record kernel
+    if ((rec_len == 0 && !items_ok(n_rec)) || !flags_ok(flags))   // empty records: one-lane-per-record kernel
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
@@ -158,18 +213,8 @@ int digest_fixed(FixedLauncher launch, size_t dig_len, const void *data, uint32_
             return fail_hip("kernel launch", e);
         return finish(s, flags);
     }
-    const size_t in_bytes = size_t(rec_len) * n_rec;
-    const size_t off_out = align_up(in_bytes, 256);
-    uint8_t *ws = static_cast<uint8_t *>(workspace(off_out + dig_len * n_rec, &e));
-    if (!ws)
-        return fail_hip("device workspace", e);
-    if (in_bytes && (e = hipMemcpyAsync(ws, data, in_bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
-        return fail_hip("hipMemcpyAsync H2D", e);
-    if ((e = launch(ws, rec_len, n_rec, ws + off_out, s)) != hipSuccess)
-        return fail_hip("kernel launch", e);
-    if ((e = hipMemcpyAsync(digests, ws + off_out, dig_len * n_rec, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return fail_hip("hipMemcpyAsync D2H", e);
-    return finish(s, flags & ~BRB_BATCH_ASYNC);
+    return brb_host::digest_fixed(launch, dig_len, static_cast<const uint8_t *>(data), rec_len, n_rec,
+                                  static_cast<uint8_t *>(digests), flags, s);
 }
 
 int digest_var(VarLauncher launch, size_t dig_len, const void *data, const uint64_t *offsets,
@@ -182,10 +227,15 @@ int digest_var(VarLauncher launch, size_t dig_len, const void *data, const uint6
         set_err("NULL data, offsets, lengths or digests");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n_rec))
+    if (!items_ok(n_rec) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES)   // contiguous record ranges, one per device
+        return brb_host::split_devices(n_rec, [&](int, uint64_t lo, uint64_t hi) {
+            return digest_var(launch, dig_len, data, offsets + lo, lengths + lo, hi - lo,
+                              static_cast<uint8_t *>(digests) + lo * dig_len, flags & ~BRB_BATCH_ALL_DEVICES, nullptr);
+        });
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
@@ -252,6 +302,8 @@ int blowfish_batch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n
         set_err("NULL ctx or words");
         return BRB_BATCH_BADARG;
     }
+    if (!flags_ok(flags))
+        return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -263,21 +315,7 @@ int blowfish_batch(const BRB_BLOWFISH_CTX *ctx, unsigned long *words, uint64_t n
             return fail_hip("kernel launch", e);
         return finish(s, flags);
     }
-    const size_t ctx_bytes = align_up(sizeof(BRB_BLOWFISH_CTX), 256);
-    const size_t w_bytes = size_t(16) * n_blocks;
-    uint8_t *ws = static_cast<uint8_t *>(workspace(ctx_bytes + w_bytes, &e));
-    if (!ws)
-        return fail_hip("device workspace", e);
-    if ((e = hipMemcpyAsync(ws, ctx, sizeof(BRB_BLOWFISH_CTX), hipMemcpyHostToDevice, s)) != hipSuccess)
-        return fail_hip("hipMemcpyAsync H2D", e);
-    if ((e = hipMemcpyAsync(ws + ctx_bytes, words, w_bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
-        return fail_hip("hipMemcpyAsync H2D", e);
-    if ((e = brb::launch_blowfish(reinterpret_cast<const uint64_t *>(ws), reinterpret_cast<uint64_t *>(ws + ctx_bytes),
-                                  n_blocks, decrypt, s)) != hipSuccess)
-        return fail_hip("kernel launch", e);
-    if ((e = hipMemcpyAsync(words, ws + ctx_bytes, w_bytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return fail_hip("hipMemcpyAsync D2H", e);
-    return finish(s, flags & ~BRB_BATCH_ASYNC);
+    return brb_host::blowfish(ctx, reinterpret_cast<uint64_t *>(words), n_blocks, decrypt, flags, s);
 }
 
 // ---- host-mode staging for the multi-buffer (RC4) batches --------------------------------------
@@ -768,6 +806,48 @@ int BRB_CryptoGPU_Available(void)
 {
     t_err.clear();
     return device_ok() == BRB_BATCH_OK ? 1 : 0;
+}
+
+int BRB_CryptoGPU_DeviceCount(void)
+{
+    t_err.clear();
+    const int n = brb_api::device_count();
+    if (n == 0)
+        (void)device_ok();   // sets the reason
+    return n;
+}
+
+int BRB_CryptoGPU_SetDevice(int dev)
+{
+    t_err.clear();
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    if (dev < 0 || dev >= brb_api::device_count()) {
+        set_err("device %d out of range (%d visible)", dev, brb_api::device_count());
+        return BRB_BATCH_BADARG;
+    }
+    hipError_t e = hipSetDevice(dev);
+    return e == hipSuccess ? BRB_BATCH_OK : fail_hip("hipSetDevice", e);
+}
+
+int BRB_CryptoGPU_GetDevice(void)
+{
+    t_err.clear();
+    if (device_ok() != BRB_BATCH_OK)
+        return -1;
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) {
+        fail_hip("hipGetDevice", e);
+        return -1;
+    }
+    return dev;
+}
+
+void BRB_CryptoGPU_ThreadCleanup(void)
+{
+    t_err.clear();
+    brb_api::release_thread_resources();
 }
 
 const char *BRB_CryptoGPU_LastError(void)

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -27,6 +28,7 @@
 #include "brb_crypto.h"
 #include "brb_kernels.h"
 
+using brb_api::DeviceGuard;
 using brb_api::fail_hip;
 using brb_api::set_err;
 
@@ -64,8 +66,8 @@ thread_local HostRange t_last[kHits];            // this thread's last hits, val
 thread_local unsigned t_next = 0;
 thread_local uint64_t t_last_gen = 0;
 
-// Device address of [p, p + len) if it lies in page-locked memory the GPU can read.
-bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
+// Device address of [p, p + len) if it lies in page-locked memory the GPU can read (device `dev`).
+bool host_to_device(const void *p, uint64_t len, uintptr_t *d, int dev)
 {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     // a receive loop submits buffers from the same few regions (reads and writes alternate between
@@ -96,7 +98,8 @@ bool host_to_device(const void *p, uint64_t len, uintptr_t *d)
         }
     }
     void *dp = nullptr;                      // page-locked by HIP itself (hipHostMalloc)
-    if (hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) == hipSuccess && dp) {
+    DeviceGuard g(dev);
+    if (g.error() == hipSuccess && hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) == hipSuccess && dp) {
         *d = reinterpret_cast<uintptr_t>(dp);
         return true;
     }
@@ -193,6 +196,10 @@ struct BRB_TransformBatcher {
     int n_rounds = 1;          // 2 when pipelined
     int cur = 0;               // the round Read/Write fill
     int dev = 0;
+    // test hook (BRB_TEST_BATCHER_FAULT=k, read at Create): the k-th kernel launch of a round is
+    // reported as failed without running, so the tests can check that a failed round is dropped
+    // exactly once (the groups launched before it ran; nothing runs twice)
+    int fault_launch = -1;
     hipStream_t stream = nullptr;          // kernels (and Enable/GetState), in round order
     // Pipelined: round k+1's H2D and round k's D2H run on their own streams, so the two copy
     // directions overlap each other and the kernels.  One-round batchers use `stream` for all.
@@ -205,7 +212,7 @@ struct BRB_TransformBatcher {
 
     ~BRB_TransformBatcher()
     {
-        (void)hipSetDevice(dev);
+        DeviceGuard g(dev);
         for (hipStream_t q : {s_h2d, s_d2h, stream})
             if (q)
                 (void)hipStreamSynchronize(q);
@@ -267,6 +274,8 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     b->zc = zc;
     b->n_rounds = pipelined ? 2 : 1;
     b->enabled.assign(max_conns, 0);
+    if (const char *f = getenv("BRB_TEST_BATCHER_FAULT"))
+        b->fault_launch = atoi(f);
     // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
     b->max_items = 4 * uint64_t(max_conns);
     b->out_cap = up(max_round_bytes + kHdr * b->max_items, kAlign);
@@ -309,7 +318,10 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
     BRB_RC4_State st;
     memset(&st, 0, sizeof(st));              // ev_kq_aio_transform.c:78 memset of the crypto states
     BRB_RC4_Init(&st, static_cast<const unsigned char *>(key), key_sz);
+    DeviceGuard g(b->dev);
     hipError_t e;
+    if ((e = g.error()) != hipSuccess)
+        return fail_hip("hipSetDevice", e);
     for (int op = 0; op < 2; op++)
         if ((e = hipMemcpyAsync(b->state(conn, op), &st, sizeof(st), hipMemcpyHostToDevice, b->stream)) != hipSuccess)
             return fail_hip("hipMemcpyAsync H2D", e);
@@ -372,7 +384,7 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
     it = Item{conn, op, in_off, len, out_off, out_len, salt, 0};
     if (b->zc) {
         uintptr_t d = 0;
-        if (len && !host_to_device(data, len, &d)) {
+        if (len && !host_to_device(data, len, &d, b->dev)) {
             it.conn = kHole;   // this thread's next buffer takes the slot and the bytes
             set_err("zero-copy batcher: buffer is not in page-locked memory (BRB_CryptoGPU_HostRegister)");
             return BRB_BATCH_BADARG;
@@ -411,8 +423,9 @@ static size_t collect(BRB_TransformBatcher *b, Round &R)
 }
 
 // Enqueues round R on the batcher's stream: metadata, H2D, the kernels, D2H, then R.done.  Nothing
-// waits here; the stream keeps rounds (and so every connection's RC4 stream) in order.
-static int launch_round(BRB_TransformBatcher *b, Round &R)
+// waits here; the stream keeps rounds (and so every connection's RC4 stream) in order.  *started is
+// set once the first copy has been enqueued.
+static int enqueue_round(BRB_TransformBatcher *b, Round &R, bool *started)
 {
     hipError_t e;
     // arena bytes past the last successful reservation belong to failed ones: not copied
@@ -480,6 +493,7 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
     const bool split = b->s_h2d != nullptr;
     // the arena's previous round was delivered (its done event waited on) before it was refilled
     hipStream_t sh = split ? b->s_h2d : s;
+    *started = true;
     if ((!b->zc && (e = hipMemcpyAsync(R.d_in, R.h_in, in_used, hipMemcpyHostToDevice, sh)) != hipSuccess) ||
         (e = hipMemcpyAsync(R.d_meta, R.h_meta, m, hipMemcpyHostToDevice, sh)) != hipSuccess)
         return fail_hip("hipMemcpyAsync H2D", e);
@@ -496,6 +510,8 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
         const uint32_t *lens = reinterpret_cast<const uint32_t *>(R.d_meta + g.o_lens);
         const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_ooffs);
         const uint64_t *salts = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_salts);
+        if (int64_t(gi) == b->fault_launch)
+            return fail_hip("kernel launch (BRB_TEST_BATCHER_FAULT)", hipErrorLaunchFailure);
         if (b->zc) {
             // inputs read in place over PCIe, outputs written into the page-locked output arena
             if (b->algo == BRB_CRYPTO_FUNC_RC4) {
@@ -536,14 +552,38 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
     return BRB_BATCH_OK;
 }
 
+// enqueue_round, and on failure drop the round: it is never retried, because the groups enqueued
+// before the failure may already have advanced their connections' RC4 states and running them again
+// would advance those states twice.  The streams are drained first, so no copy still reads an arena
+// that the next round refills.  Returns BRB_BATCH_OK or BRB_BATCH_NOT_DONE (reason in LastError).
+static int launch_round(BRB_TransformBatcher *b, Round &R)
+{
+    bool started = false;
+    if (enqueue_round(b, R, &started) == BRB_BATCH_OK)
+        return BRB_BATCH_OK;
+    if (started)
+        for (hipStream_t q : {b->s_h2d, b->s_d2h, b->stream})
+            if (q)
+                (void)hipStreamSynchronize(q);
+    const std::string why = brb_api::t_err;
+    set_err("%s; round of %zu buffers dropped%s", why.c_str(), R.items.size(),
+            started ? " (groups launched before the failure have advanced their connections' states)" : "");
+    R.reset();
+    return BRB_BATCH_NOT_DONE;
+}
+
 // Waits for round R and hands every result back in submission order; the k-th read item of a
-// group has valid flag k of that group.  Returns the number of buffers delivered, or -1.
+// group has valid flag k of that group.  Returns the number of buffers delivered, or -1 when the
+// round failed on the device (it is dropped without callbacks; reason in LastError).
 static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user)
 {
     hipError_t e;
     if ((e = hipEventSynchronize(R.done)) != hipSuccess) {
+        fail_hip("round completion", e);
+        const std::string why = brb_api::t_err;
+        set_err("%s; round of %zu buffers dropped", why.c_str(), R.items.size());
         R.reset();
-        return fail_hip("round completion", e);
+        return -1;
     }
     std::vector<uint32_t> next_in_group(R.group_valid.size(), 0);
     for (const Item &it : R.items) {
@@ -580,15 +620,16 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         set_err("NULL batcher");
         return BRB_BATCH_BADARG;
     }
+    DeviceGuard g(b->dev);
     hipError_t e;
-    if ((e = hipSetDevice(b->dev)) != hipSuccess)
+    if ((e = g.error()) != hipSuccess)
         return fail_hip("hipSetDevice", e);
     int64_t total = 0;
     Round &prev = b->r[b->cur ^ (b->n_rounds - 1)];
     if (b->n_rounds == 2 && prev.in_flight) {   // the round FlushAsync left running comes first
         const int64_t n = deliver_round(b, prev, done, user);
         if (n < 0)
-            return n;
+            return BRB_BATCH_NOT_DONE;          // the current round stays pending
         total += n;
     }
     Round &R = b->r[b->cur];
@@ -596,14 +637,10 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         R.reset();
         return total;
     }
-    int rc = launch_round(b, R);
-    if (rc != BRB_BATCH_OK) {
-        if (rc < 0)   // enqueue failed: the round is lost, the stream may hold part of it
-            R.reset();
-        return rc;
-    }
+    if (launch_round(b, R) != BRB_BATCH_OK)
+        return BRB_BATCH_NOT_DONE;
     const int64_t n = deliver_round(b, R, done, user);
-    return n < 0 ? n : total + n;
+    return n < 0 ? BRB_BATCH_NOT_DONE : total + n;
 }
 
 int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
@@ -615,24 +652,24 @@ int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDon
     }
     if (b->n_rounds == 1)
         return BRB_TransformBatcherFlush(b, done, user);
+    DeviceGuard g(b->dev);
     hipError_t e;
-    if ((e = hipSetDevice(b->dev)) != hipSuccess)
+    if ((e = g.error()) != hipSuccess)
         return fail_hip("hipSetDevice", e);
     Round &R = b->r[b->cur], &prev = b->r[b->cur ^ 1];
     if (collect(b, R) == 0) {
         R.reset();
-    } else {
-        // enqueue this round first so the GPU has it while the previous round's callbacks run
-        int rc = launch_round(b, R);
-        if (rc != BRB_BATCH_OK) {
-            if (rc < 0)
-                R.reset();
-            return rc;
-        }
+    } else if (launch_round(b, R) != BRB_BATCH_OK) {
+        // enqueue this round first so the GPU has it while the previous round's callbacks run; a
+        // failed one is dropped, and the previous round (if running) is delivered by the next flush
+        return BRB_BATCH_NOT_DONE;
     }
     if (R.in_flight)
         b->cur ^= 1;   // Read/Write now fill the other arena (the previous round's, once delivered)
-    return prev.in_flight ? deliver_round(b, prev, done, user) : 0;
+    if (!prev.in_flight)
+        return 0;
+    const int64_t n = deliver_round(b, prev, done, user);
+    return n < 0 ? BRB_BATCH_NOT_DONE : n;
 }
 
 }  // extern "C"
@@ -686,8 +723,10 @@ int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op,
         set_err("bad batcher, connection or op");
         return BRB_BATCH_BADARG;
     }
+    DeviceGuard g(b->dev);
     hipError_t e;
-    if ((e = hipMemcpyAsync(out, b->state(conn, op), sizeof(*out), hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
+    if ((e = g.error()) != hipSuccess ||
+        (e = hipMemcpyAsync(out, b->state(conn, op), sizeof(*out), hipMemcpyDeviceToHost, b->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(b->stream)) != hipSuccess)
         return fail_hip("state copy", e);
     return BRB_BATCH_OK;

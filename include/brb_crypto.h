@@ -116,9 +116,19 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
                                       is device memory (HBM-resident); nothing crosses PCIe       */
 #define BRB_BATCH_ASYNC     0x2u   /* with BRB_BATCH_DEVICE: enqueue on `hip_stream` and return
                                       without waiting; the caller synchronises the stream         */
+#define BRB_BATCH_ALL_DEVICES 0x4u /* host mode only (BRB_MD5BatchFixed, BRB_MD5Batch,
+                                      BrbSha1_BatchFixed, BrbSha1_Batch, BRB_Blowfish_*Batch):
+                                      split the records (blocks) into contiguous ranges
+                                      [g*n/G, (g+1)*n/G), one per visible device g < G, run them
+                                      concurrently and return when all are done (SURVEY §8(e):
+                                      no collective).  With BRB_BATCH_DEVICE: -1.                   */
 
-/* `hip_stream` is a hipStream_t (NULL = the legacy default stream of the current device).
- * Work runs on the caller's current HIP device (hipSetDevice / torch.cuda.set_device). */
+/* Device mode: `hip_stream` is a hipStream_t (NULL = the legacy default stream of the current
+ * device) and the work runs on the caller's current HIP device (BRB_CryptoGPU_SetDevice,
+ * hipSetDevice or torch.cuda.set_device).  Host mode: the call runs on the caller's current device
+ * (or on every device with BRB_BATCH_ALL_DEVICES), copies straight from and to the caller's memory
+ * (pageable or page-locked) in chunks so that copies in both directions overlap the kernels, and
+ * returns when the results are in host memory; `hip_stream` is not used. */
 
 /* MD5 of n_rec records of rec_len bytes each, stored back to back: record i is
  * data[i*rec_len .. (i+1)*rec_len).  digests[i] = BRB_MD5Init/Update/Final of record i. */
@@ -228,8 +238,12 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
  * chunks, so a round shared by T threads may report full up to T chunks (64 buffers, 128 KiB) early. */
 int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
 int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
-/* Runs the round; returns the number of buffers delivered, or -1 / 0 as the batch calls do.  On a
- * pipelined batcher it first delivers the round FlushAsync left running, so Flush drains everything. */
+/* Runs the round; returns the number of buffers delivered, -1 for bad arguments, or 0 with LastError
+ * set on a device error.  A round that fails on the device is dropped without callbacks and never
+ * re-run (kernels launched before the failure may have advanced their connections' states; running
+ * them again would advance them twice).  On a pipelined batcher Flush first delivers the round
+ * FlushAsync left running, so Flush drains everything.  A batcher's calls run on the device it was
+ * created on and leave the calling thread's current device unchanged. */
 int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
 /* Pipelined rounds: enqueues the current round and returns without waiting for it, after delivering
  * the previous round (if one is running) in submission order; Read/Write then fill the other arena.
@@ -280,6 +294,17 @@ int BRB_MemBufferDecrypt(void *buf, unsigned long size, unsigned int seed, unsig
 /* ---- runtime ---------------------------------------------------------------------------- */
 /* 1 if a HIP device is usable from this process, else 0 (reason in LastError). */
 int BRB_CryptoGPU_Available(void);
+/* Number of visible HIP devices (probed once per process); 0 if none (reason in LastError). */
+int BRB_CryptoGPU_DeviceCount(void);
+/* Makes `dev` the calling thread's current device for the batch calls, so a C caller that does not
+ * link HIP itself can drive several GPUs (e.g. one event thread per GPU): 1 = done, 0 = no device /
+ * HIP error, -1 = dev out of range. */
+int BRB_CryptoGPU_SetDevice(int dev);
+/* The calling thread's current device, or -1 (reason in LastError). */
+int BRB_CryptoGPU_GetDevice(void);
+/* Frees the calling thread's host-mode scratch (device workspaces, streams, events) now instead of
+ * at thread exit.  Call it with no batch call of this thread running. */
+void BRB_CryptoGPU_ThreadCleanup(void);
 /* Last error of the calling thread ("" if none). */
 const char *BRB_CryptoGPU_LastError(void);
 /* Page-lock [p, p + len) for the GPU (hipHostRegister, mapped) so that zero-copy batchers can read

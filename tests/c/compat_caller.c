@@ -9,7 +9,9 @@
  *   - MemBuffer Blowfish ECB over word pairs                     (data/core/mem_buf.c:1528-1539)
  *   - RC4 connection streams: Init per direction, Crypt per buffer (ev_kq_aio_transform.c:89-90,273,282)
  *   - then the batch surface on the same records, which must agree with the compat results
- *     (returns 0 with a reason when no GPU is present; it never computes on the CPU).
+ *     (returns 0 with a reason when no GPU is present; it never computes on the CPU),
+ *   - and the multi-device runtime: BRB_CryptoGPU_DeviceCount / SetDevice per device, and one
+ *     batch split over every device with BRB_BATCH_ALL_DEVICES.
  *
  * Output: one line per check, "name value", parsed by tests/test_abi.py.
  */
@@ -120,5 +122,34 @@ int main(void)
     uint32_t len0 = RLEN;
     rc = BRB_RC4_CryptBatch(&bst, recs, bc, &off0, &len0, 1, BRB_BATCH_HOST, NULL);
     printf("batch_rc4_eq %d\n", rc == 1 && memcmp(bc, c1, RLEN) == 0 && memcmp(&bst, &wst, sizeof(bst)) == 0);
+
+    /* several GPUs from one process without linking HIP (the kqueue daemon's event threads, one
+     * per GPU): device count, per-thread device selection, and one batch split over every device */
+    int ndev = BRB_CryptoGPU_DeviceCount();
+    printf("devices %d\n", ndev);
+    int per_dev_ok = ndev > 0;
+    for (int g = 0; g < ndev; g++) {
+        if (BRB_CryptoGPU_SetDevice(g) != BRB_BATCH_OK) {
+            per_dev_ok = 0;
+            break;
+        }
+        memset(dig16, 0, sizeof(dig16));
+        rc = BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_HOST, NULL);
+        per_dev_ok &= rc == 1 && memcmp(dig16, ref16, sizeof(ref16)) == 0 && BRB_CryptoGPU_GetDevice() == g;
+    }
+    (void)BRB_CryptoGPU_SetDevice(0);
+    printf("per_device_md5_eq %d\n", per_dev_ok);
+    memset(dig16, 0, sizeof(dig16));
+    rc = BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_HOST | BRB_BATCH_ALL_DEVICES, NULL);
+    printf("all_devices_md5_eq %d\n", rc == 1 && memcmp(dig16, ref16, sizeof(ref16)) == 0);
+    memcpy(w, w0, sizeof(w));
+    rc = BRB_Blowfish_EncryptBatch(&bf, w, 32, BRB_BATCH_HOST | BRB_BATCH_ALL_DEVICES, NULL);
+    printf("all_devices_bf_eq %d\n", rc == 1 && memcmp(w, enc, sizeof(enc)) == 0);
+    printf("set_device_out_of_range %d\n", BRB_CryptoGPU_SetDevice(ndev));
+    printf("all_devices_with_device_ptrs %d\n",
+           BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_DEVICE | BRB_BATCH_ALL_DEVICES, NULL));
+    BRB_CryptoGPU_ThreadCleanup();
+    rc = BRB_MD5BatchFixed(recs, RLEN, NREC, dig16, BRB_BATCH_HOST, NULL);
+    printf("after_cleanup_md5_eq %d\n", rc == 1 && memcmp(dig16, ref16, sizeof(ref16)) == 0);
     return 0;
 }

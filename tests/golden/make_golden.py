@@ -12,6 +12,10 @@ Sources, in order of authority (DESIGN.md "Oracle"):
   * the oracle restatement (oracle/brb_oracle.c) for what no external source pins: the HIGH 32 bits
     of the reference's 64-bit Blowfish words, the SHA-1 in-place mutation bytes and the MemBuffer
     wrappers.  These are marked "source": "oracle" -- regression fixtures, not pins.
+  * for the 64-bit Blowfish words, a second, independent derivation written here: Python big
+    integers reduced mod 2^64 (the LP64 `unsigned long` of blowfish.c:312-462), with the pi tables
+    computed by the Chudnovsky series (the oracle uses BBP digit extraction, the product's header
+    Machin's formula).  blowfish64.json is written only if both derivations agree on every word.
 
 The reference itself cannot be built here (libbrb_data.h needs <bsd/string.h>, absent; stand-in
 headers are not allowed), so no fixture comes from running reference code.
@@ -93,6 +97,120 @@ def libcrypto_rc4(key: bytes, data: bytes) -> bytes:
     return out.raw[: len(data)]
 
 
+# ---- independent big-integer restatement of blowfish.c (second derivation of the 64-bit words) ----
+M64 = (1 << 64) - 1
+
+
+def pi_words_chudnovsky(n_words: int) -> list:
+    """The first n_words 32-bit words of pi's fractional part (0x243F6A88, ...), from the Chudnovsky
+    series by binary splitting, in integers only."""
+    bits = 32 * n_words + 64                     # 64 guard bits
+    terms = (bits * 30103 // 100000) // 14 + 3   # each term adds ~14.18 decimal digits
+
+    def split(a, b):
+        if b - a == 1:
+            if a == 0:
+                p = q = 1
+            else:
+                p = (6 * a - 5) * (2 * a - 1) * (6 * a - 1)
+                q = a * a * a * 10939058860032000
+            t = p * (13591409 + 545140134 * a)
+            return p, q, (-t if a & 1 else t)
+        m = (a + b) // 2
+        p1, q1, t1 = split(a, m)
+        p2, q2, t2 = split(m, b)
+        return p1 * p2, q1 * q2, q2 * t1 + p1 * t2
+
+    import math
+    _, q, t = split(0, terms)
+    pi_scaled = q * 426880 * math.isqrt(10005 << (2 * bits)) // t      # pi * 2^bits
+    frac = (pi_scaled - (3 << bits)) >> 64
+    return [(frac >> (32 * (n_words - 1 - i))) & 0xFFFFFFFF for i in range(n_words)]
+
+
+class BigIntBlowfish:
+    """BRB_Blowfish_Init/Encrypt/Decrypt (blowfish.c:312-443) with _F (:445-462) on LP64 words:
+    every `unsigned long` operation is a Python integer operation reduced mod 2^64."""
+
+    PI = None
+
+    def __init__(self, key: bytes, key_len: int | None = None):
+        if BigIntBlowfish.PI is None:
+            BigIntBlowfish.PI = pi_words_chudnovsky(18 + 4 * 256)
+        pi = BigIntBlowfish.PI
+        key_len = len(key) if key_len is None else key_len
+        self.S = [list(pi[18 + 256 * i: 18 + 256 * (i + 1)]) for i in range(4)]
+        self.P = []
+        j = 0
+        for i in range(18):
+            data = 0
+            for _ in range(4):
+                data = ((data << 8) | key[j]) & M64
+                j += 1
+                if j >= key_len:
+                    j = 0
+            self.P.append(pi[i] ^ data)
+        xl = xr = 0
+        for i in range(0, 18, 2):
+            xl, xr = self.encrypt(xl, xr)
+            self.P[i], self.P[i + 1] = xl, xr
+        for i in range(4):
+            for j in range(0, 256, 2):
+                xl, xr = self.encrypt(xl, xr)
+                self.S[i][j], self.S[i][j + 1] = xl, xr
+
+    def f(self, x: int) -> int:
+        a, b, c, d = (x >> 24) & 0xFF, (x >> 16) & 0xFF, (x >> 8) & 0xFF, x & 0xFF
+        y = (self.S[0][a] + self.S[1][b]) & M64
+        y ^= self.S[2][c]
+        return (y + self.S[3][d]) & M64
+
+    def encrypt(self, xl: int, xr: int):
+        for i in range(16):
+            xl ^= self.P[i]
+            xr ^= self.f(xl)
+            xl, xr = xr, xl
+        xl, xr = xr, xl
+        return xl ^ self.P[17], xr ^ self.P[16]
+
+    def decrypt(self, xl: int, xr: int):
+        for i in range(17, 1, -1):
+            xl ^= self.P[i]
+            xr ^= self.f(xl)
+            xl, xr = xr, xl
+        xl, xr = xr, xl
+        return xl ^ self.P[0], xr ^ self.P[1]
+
+    def ctx_bytes(self) -> bytes:
+        """The 8336-byte BRB_BLOWFISH_CTX image (LP64, little-endian)."""
+        return b"".join(v.to_bytes(8, "little") for v in self.P + [w for row in self.S for w in row])
+
+
+def check_blowfish64(bf: dict) -> None:
+    """Asserts that the big-integer derivation reproduces every word of a blowfish64.json dict."""
+    for c in bf["contexts"]:
+        b = BigIntBlowfish(bytes.fromhex(c["key"]))
+        assert hashlib.sha256(b.ctx_bytes()).hexdigest() == c["sha256"], c["key"]
+        assert [hex(v) for v in b.P] == c["P"], c["key"]
+        # SURVEY §8 a11: the carries make most entries wider than 32 bits, "up to 50 significant
+        # bits" for the keys the survey ran; a 56-byte key reaches 51.  Each context's measured
+        # width is part of the fixture.
+        words = b.P + [w for row in b.S for w in row]
+        assert max(w.bit_length() for w in words) == c["max_bits"], c["key"]
+        assert sum(1 for w in words if w >> 32) > len(words) // 2, c["key"]
+    g = bf["cfg4"]
+    b = BigIntBlowfish(bytes.fromhex(g["key"]))
+    words = [int(v) for v in workload.gen_words(g["seed"], 2 * g["pairs"])]
+    assert hashlib.sha256(np.array(words, np.uint64).tobytes()).hexdigest() == g["plain_sha256"]
+    ct = []
+    for i in range(g["pairs"]):
+        xl, xr = b.encrypt(words[2 * i], words[2 * i + 1])
+        assert b.decrypt(xl, xr) == (words[2 * i], words[2 * i + 1])
+        ct += [xl, xr]
+    assert hashlib.sha256(np.array(ct, np.uint64).tobytes()).hexdigest() == g["cipher_sha256"]
+    assert [hex(v) for v in ct[:16]] == g["cipher_first8"]
+
+
 def dump(name, obj):
     with open(os.path.join(OUT, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -123,10 +241,15 @@ def main():
         edge.append({"len": n, "record": 7, "md5": hashlib.md5(rec).hexdigest(),
                      "sha1": hashlib.sha1(rec).hexdigest(), "first8": rec[:8].hex()})
     cfgs = {}
-    for c in (1, 2, 3):
+    for c in (1, 2, 3, 5):
         cfg = workload.CONFIGS[c]
         n, L = cfg["records"], cfg["rec_len"]
-        idx = sorted(set(list(range(min(64, n))) + list(range(max(0, n - 64), n))))
+        idx = set(list(range(min(64, n))) + list(range(max(0, n - 64), n)))
+        if c == 5:   # both ends of every GPU's shard: records [g N/8, (g+1) N/8)
+            for g in range(8):
+                r0, r1 = workload.shard(n, g, 8)
+                idx |= {r0, r0 + 1, r1 - 2, r1 - 1}
+        idx = sorted(idx)
         recs = []
         for r in idx:
             b = workload.gen_records(workload.SEEDS[c], r, 1, L).tobytes()
@@ -140,7 +263,9 @@ def main():
     for key in (b"TESTKEY", workload.CFG4_KEY, bytes(range(56))):
         c = oracle.bf_init(key)
         raw = oracle.bf_ctx_bytes(c)
+        words = list(c.P) + [c.S[i][j] for i in range(4) for j in range(256)]
         bf["contexts"].append({"key": key.hex(), "sha256": hashlib.sha256(raw).hexdigest(),
+                               "max_bits": max(int(w).bit_length() for w in words),
                                "P": [hex(v) for v in c.P], "S0_first4": [hex(c.S[0][i]) for i in range(4)],
                                "S3_last4": [hex(c.S[3][i]) for i in range(252, 256)]})
     c = oracle.bf_init(workload.CFG4_KEY)
@@ -150,6 +275,9 @@ def main():
                   "plain_sha256": hashlib.sha256(words.tobytes()).hexdigest(),
                   "cipher_sha256": hashlib.sha256(ct.tobytes()).hexdigest(),
                   "cipher_first8": [hex(int(v)) for v in ct[:16]]}
+    check_blowfish64(bf)     # second derivation: every word reproduced by the big-integer restatement
+    bf["second_derivation"] = ("tests/golden/make_golden.py BigIntBlowfish: Python big integers mod 2^64, pi by "
+                               "Chudnovsky; reproduces every context and cipher word above")
     dump("blowfish64.json", bf)
 
     msg = bytearray(workload.gen_records(seed, 3, 1, 200).tobytes())

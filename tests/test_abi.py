@@ -1,10 +1,12 @@
 """The drop-in boundary: libbrb_crypto_gpu.so loads, exports exactly include/brb_crypto.h, links
 into an unchanged C caller, and the batch surface refuses (never falls back) without a GPU."""
+import ctypes
 import hashlib
 import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -127,3 +129,24 @@ def test_batch_refuses_oversized_item_counts(brb):
     assert L.BRB_MD5BatchFixed(b, 0, n, b, 0, None) == -1
     assert L.BRB_TransformBatcherCreate(1 << 31, 1 << 20, 1) is None
     assert b"max_conns" in L.BRB_CryptoGPU_LastError()
+
+
+def test_multi_device_runtime_without_gpu(brb):
+    """The multi-device runtime (BRB_CryptoGPU_DeviceCount / SetDevice / GetDevice / ThreadCleanup,
+    BRB_BATCH_ALL_DEVICES) checks its arguments before any device work, so this runs here."""
+    L = brb.lib()
+    b = ctypes.create_string_buffer(64 * 16)
+    flags = brb.BATCH_DEVICE | brb.BATCH_ALL_DEVICES
+    assert L.BRB_MD5BatchFixed(b, 64, 4, b, flags, None) == -1
+    assert b"ALL_DEVICES" in L.BRB_CryptoGPU_LastError()
+    assert L.BrbSha1_Batch(b, b, b, 4, b, flags, None) == -1
+    assert L.BRB_Blowfish_DecryptBatch(b, b, 4, flags, None) == -1
+    L.BRB_CryptoGPU_ThreadCleanup()
+    if brb.gpu_available():
+        assert L.BRB_CryptoGPU_DeviceCount() >= 1
+        return
+    assert L.BRB_CryptoGPU_DeviceCount() == 0 and L.BRB_CryptoGPU_LastError()
+    assert L.BRB_CryptoGPU_SetDevice(0) == 0 and L.BRB_CryptoGPU_GetDevice() == -1
+    data = np.zeros(64 * 4, np.uint8)
+    with pytest.raises(RuntimeError, match="returned 0"):
+        brb.md5_batch_fixed(data, 64, all_devices=True)

@@ -219,3 +219,30 @@ def test_pipelined_edges(brb, orc, torch_dev):
     assert b.read(0, b"left running") == 1
     assert b.flush_async() == []
     b.close()                                    # waits for the running round
+
+
+def test_failed_round_is_dropped_once(brb, orc, torch_dev, monkeypatch):
+    """A round whose enqueue fails part-way is dropped, never re-run (transform_batcher.hip
+    launch_round).  BRB_TEST_BATCHER_FAULT=1 makes the second kernel launch of a round report a
+    failure without running: connection 0 has two read buffers (sub-rounds 0 and 1), so group 0
+    (its first buffer) runs and group 1 does not.  Flush returns 0 with the reason; the next Flush has
+    nothing to run; the state shows the first buffer applied exactly once."""
+    monkeypatch.setenv("BRB_TEST_BATCHER_FAULT", "1")
+    b = brb.TransformBatcher(4, 1 << 20, 1)
+    monkeypatch.delenv("BRB_TEST_BATCHER_FAULT")
+    key = b"faultkey"
+    b.enable(0, key)
+    st = orc.rc4_init(key)
+    first = bytes(range(200))
+    assert b.read(0, first) == 1 and b.read(0, bytes(100)) == 1
+    with pytest.raises(RuntimeError, match="dropped"):
+        b.flush()
+    assert b.flush() == []                         # the failed round is gone, nothing re-runs
+    st_once, _ = orc.rc4_crypt(st, first)
+    assert b.state(0, 0) == st_once                # group 0 ran once; group 1 never ran
+    # the batcher keeps working: the next buffer continues from that state
+    assert b.read(0, first) == 1
+    got = b.flush()
+    st_twice, want = orc.rc4_crypt(st_once, first)
+    assert got == [(0, 0, want, 1)] and b.state(0, 0) == st_twice
+    b.close()

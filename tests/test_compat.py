@@ -50,6 +50,31 @@ def test_md5_context_bytes_match_oracle(brb, orc):
     assert bytes(c)[:104 + 33] == bytes(o)[:104 + 33]
 
 
+def test_cfg1_compat_md5_1mib(brb, golden):
+    """BASELINE cfg1 as configured: one 1 048 576-byte buffer through the product's compat
+    BRB_MD5Init / BRB_MD5UpdateBig / BRB_MD5Final (md5.c:38-168; UpdateBig feeds Update 65 535-byte
+    pieces), against digests.json configs["1"] (hashlib) -- also as one Update and as 4 KiB Updates."""
+    cfg = golden["digests"]["configs"]["1"]
+    assert cfg["records"] == 1 and cfg["rec_len"] == 1 << 20
+    buf = workload.gen_records(cfg["seed"], 0, 1, cfg["rec_len"]).tobytes()
+    want = cfg["digests"][0]["md5"]
+    assert hashlib.md5(buf).hexdigest() == want
+    L = brb.lib()
+    c = _md5_ctx(brb)
+    L.BRB_MD5UpdateBig(ctypes.byref(c), buf, len(buf))
+    L.BRB_MD5Final(ctypes.byref(c))
+    assert bytes(c.digest).hex() == want and bytes(c.string[:32]).decode() == want
+    c = _md5_ctx(brb)
+    L.BRB_MD5Update(ctypes.byref(c), buf, len(buf))
+    L.BRB_MD5Final(ctypes.byref(c))
+    assert bytes(c.digest).hex() == want
+    c = _md5_ctx(brb)
+    for i in range(0, len(buf), 4096):
+        L.BRB_MD5Update(ctypes.byref(c), buf[i:i + 4096], 4096)
+    L.BRB_MD5Final(ctypes.byref(c))
+    assert bytes(c.digest).hex() == want and list(c.bytes) == [len(buf), 0]
+
+
 def test_md5_update_big(brb):
     data = workload.gen_records(0x5EED0001, 0, 1, 300_000).tobytes()
     c = _md5_ctx(brb)

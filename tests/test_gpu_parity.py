@@ -140,15 +140,37 @@ def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
-def test_cfg5_shard_property(brb, torch_dev):
-    """One GPU's shard of cfg5 (records [7/8 N, N)): sampled records vs hashlib."""
+def test_cfg5_full_shard(brb, orc, torch_dev, golden):
+    """cfg5 as configured: GPU 7's whole shard of the 8 388 608-record batch (records [7/8 N, N),
+    1 048 576 x 1500 B = 1.57 GB, HBM-resident), every digest against the oracle, and both ends of
+    the shard against the hashlib golden digests (tests/golden/digests.json configs["5"])."""
     n_all, L = workload.CONFIGS[5]["records"], workload.CONFIGS[5]["rec_len"]
     r0, r1 = workload.shard(n_all, 7, 8)
-    n = 65536                      # a slice of the shard keeps the host-side generator quick
-    data = workload.gen_records(workload.SEEDS[5], r1 - n, n, L)
+    n = r1 - r0
+    assert n == 1 << 20
+    data = workload.gen_records(workload.SEEDS[5], r0, n, L)
     got = brb.md5_batch_fixed(to_dev(torch_dev, data), L, n).cpu().numpy()
-    for i in np.random.default_rng(2).integers(0, n, 64):
-        assert got[i].tobytes() == hashlib.md5(data[i * L:(i + 1) * L].tobytes()).digest()
+    torch_dev.cuda.empty_cache()
+    assert np.array_equal(got, orc.md5_batch_fixed(data, L, n, threads=16))
+    seen = 0
+    for e in golden["digests"]["configs"]["5"]["digests"]:
+        if r0 <= e["r"] < r1:
+            assert got[e["r"] - r0].tobytes().hex() == e["md5"]
+            seen += 1
+    assert seen == 66                # the last 64 records of cfg5 (which end the shard) + its first two
+
+
+def test_cfg5_host_all_devices(brb, orc, golden):
+    """cfg5's split as a C caller would run it on one node: one host-mode call with
+    BRB_BATCH_ALL_DEVICES (contiguous ranges over every visible device; on a one-GPU box the split
+    degenerates to that device).  A 262 144-record slice of GPU 0's shard, every digest vs the oracle."""
+    n_all, L = workload.CONFIGS[5]["records"], workload.CONFIGS[5]["rec_len"]
+    n = 1 << 18
+    data = workload.gen_records(workload.SEEDS[5], 0, n, L)
+    got = brb.md5_batch_fixed(data, L, n, all_devices=True)
+    assert np.array_equal(got, orc.md5_batch_fixed(data, L, n, threads=16))
+    for e in golden["digests"]["configs"]["5"]["digests"][:64]:
+        assert got[e["r"]].tobytes().hex() == e["md5"]
 
 
 @pytest.mark.parametrize("rec_len", [1500, 1501])
@@ -246,6 +268,10 @@ def test_c_caller_batch_on_gpu(brb, tmp_path):
     assert res["batch_md5_rc"] == "1"
     assert res["batch_md5_eq"] == "1" and res["batch_sha1_eq"] == "1" and res["batch_bf_eq"] == "1"
     assert res["batch_rc4_eq"] == "1"
+    assert int(res["devices"]) >= 1 and res["per_device_md5_eq"] == "1"
+    assert res["all_devices_md5_eq"] == "1" and res["all_devices_bf_eq"] == "1"
+    assert res["set_device_out_of_range"] == "-1" and res["all_devices_with_device_ptrs"] == "-1"
+    assert res["after_cleanup_md5_eq"] == "1"
 
 
 def test_concurrent_host_threads(brb, orc, torch_dev):
