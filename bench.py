@@ -14,8 +14,10 @@ Honesty rules applied here:
   * roofline.achieved = bytes per launch / (HIP-event time of the timed region on the launch
     stream / K); digests of the last step are spot-checked against hashlib.
 
-Other workloads for DESIGN.md: --config 3 (1 Mi x 64 B MD5), --config 4 (1 GiB Blowfish enc+dec),
---op sha1.  Run `python bench.py --help`.
+Other workloads for DESIGN.md: --config 1 (one 1 MiB buffer through the compat BRB_MD5* calls on
+the CPU, no GPU), --config 3 (1 Mi x 64 B MD5), --config 4 (1 GiB Blowfish enc+dec), --op sha1.
+Every digest line also carries a "cfg5" object: 1 048 576 x 1500 B records per GPU (exactly
+BASELINE cfg5, 8 388 608 records, at --gpus 8).  Run `python bench.py --help`.
 """
 from __future__ import annotations
 
@@ -34,6 +36,11 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s (device-resident) + Mrecords/s over 1500B buffers at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 L3_BYTES = 256 << 20
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4                # max shader clock (MI355X_MICROARCH.md "Chip-level parameters")
+VALU_PEAK_CYC = 2.0            # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (guide, "SIMD")
+LONE_WAVE_CYC = {"md5": 4.85, "sha1": 4.54}   # one wave per SIMD: measured issue cost per VALU
+                                              # instruction (tools/mb/valu_latency.hip)
 
 
 def parse():
@@ -44,7 +51,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed warm-up steps W (default: as many as fill >= 1 s, so the GPU clock has "
                          "ramped up before the timed region)")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher"],
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B)")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
@@ -52,6 +59,7 @@ def parse():
     ap.add_argument("--two-stream", action="store_true", help="also time the steps over 2 streams")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-inclusive (PCIe) measurement")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 (1 Mi records per GPU) sub-measurement")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
@@ -66,23 +74,75 @@ def relaunch_distributed(args) -> None:
 
 
 def cpu_threads() -> int:
+    """Threads for the CPU baseline: the lease's CPU share.  On the GPU box the affinity mask shows
+    the whole host (256 CPUs) while one GPU's share is 16 (OMP_NUM_THREADS / MAX_JOBS are set to it
+    and the harness asks for pools of that size); here the container's own CPUs."""
     for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         if os.environ.get(var, "").isdigit():
             return max(1, int(os.environ[var]))
-    return max(1, min(16, os.cpu_count() or 1))
+    return max(1, len(os.sched_getaffinity(0)))
 
 
-def load_traffic(path, key):
+def core_counts(threads: int, single_core_rate: float) -> dict:
+    """`cores` = threads actually used, beside `nproc` (as printed by the tool) and the affinity
+    mask; the whole-mask figure is a LINEAR EXTRAPOLATION of the measured single-core rate, labelled
+    as such (running 256 threads would exceed the lease's CPU share)."""
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
+    except (OSError, ValueError, subprocess.SubprocessError):
+        nproc = None
+    aff = len(os.sched_getaffinity(0))
+    return {"cores": threads, "nproc": nproc, "affinity_cpus": aff,
+            "all_affinity_cpus_extrapolated": round(single_core_rate * aff, 3),
+            "cores_note": f"measured on {threads} threads (the lease's CPU share); nproc={nproc} "
+                          f"(honours OMP_NUM_THREADS); affinity mask {aff} CPUs; "
+                          "all_affinity_cpus_extrapolated = single-core rate x affinity CPUs, not measured"}
+
+
+def load_pmc(path, key):
+    """(traffic bytes, detail dict) measured by rocprofv3 --pmc for `key`, or (None, None)."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(key)
+        return d.get(key), d.get(key + "_detail")
     except (OSError, ValueError):
+        return None, None
+
+
+def traffic_fields(path, key, per_step=1):
+    t, det = load_pmc(path, key)
+    src = (det or {}).get("source")
+    return {"traffic": t * per_step if t else None,
+            "traffic_source": (f"{src}: rocprofv3 --pmc passes of an earlier run (tools/gpu_pmc.sh), not this run"
+                               if src else None)}
+
+
+def compute_fraction(path, key, launch_s, cyc_lone):
+    """roofline.compute: the VALU-issue ceiling.  insts = SQ_INSTS_VALU per dispatch (rocprofv3
+    --pmc, chip-wide sum of wave-instructions); per SIMD = insts / 1024.  frac_peak = that many
+    instructions at the SIMD's peak issue (2 cycles per wave64 instruction) and 2.4 GHz over the
+    launch time; frac_lone_wave = the same at the issue cost one wave per SIMD measured (cfg2 and
+    the one-wave-per-SIMD kernels run that way)."""
+    _, det = load_pmc(path, key)
+    if not det or "sq_insts_valu" not in det:
         return None
+    per_simd = det["sq_insts_valu"] / SIMDS
+    cyc = launch_s * CLOCK_GHZ * 1e9
+    out = {"bound": "valu-issue", "sq_insts_valu_per_launch": det["sq_insts_valu"],
+           "valu_per_simd": round(per_simd, 1), "clock_ghz": CLOCK_GHZ,
+           "peak_cycles_per_inst": VALU_PEAK_CYC, "frac_peak": round(per_simd * VALU_PEAK_CYC / cyc, 4),
+           "source": det.get("source")}
+    if cyc_lone:
+        out["lone_wave_cycles_per_inst"] = cyc_lone
+        out["frac_lone_wave"] = round(per_simd * cyc_lone / cyc, 4)
+    return out
 
 
 def main():
     args = parse()
+    if args.config == 1:          # plumbing, no GPU (BASELINE cfg1)
+        print(json.dumps(bench_cfg1(args)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "RANK" not in os.environ:
         relaunch_distributed(args)
@@ -275,7 +335,7 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     # to back, so this is the kernel time plus the ~2 us dependent-kernel boundary)
     avg_kern_s = ev_s / n_steps
     achieved = n_rank * L / avg_kern_s / 1e9
-    traffic = load_traffic(args.pmc_summary, f"cfg{cfg_id}_{args.op}")
+    pmc_key = f"cfg{cfg_id}_{args.op}"
     result = {
         "metric": METRIC,
         "value": round(gib_s, 2),
@@ -297,9 +357,11 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "mrecords_per_s": round(mrec_s, 3),
         "streams": n_streams,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), **traffic_fields(args.pmc_summary, pmc_key),
                      "launch_us_avg": round(avg_kern_s * 1e6, 2), "bytes_per_launch": n_rank * L,
-                     "timing": "HIP events on the launch stream around the K back-to-back steps / K"},
+                     "timing": "HIP events on the launch stream around the K back-to-back steps / K",
+                     "compute": compute_fraction(args.pmc_summary, pmc_key, avg_kern_s,
+                                                 LONE_WAVE_CYC.get(args.op) if n_rank <= 65536 else None)},
     }
     if wall2 is not None:
         result["two_stream_throughput"] = {
@@ -307,29 +369,100 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
             "mrecords_per_s": round(n_global * n_steps / wall2 / 1e6, 3),
             "note": "same K steps alternating over 2 HIP streams (2 batches in flight)"}
     if world == 1 and not args.no_pcie:
-        result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, dev, stream, log)
+        result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, log)
+    del bufs, outs
+    torch.cuda.empty_cache()
+    if cfg_id == 2 and args.op == "md5" and not args.no_cfg5 and not args.records_per_gpu:
+        result["cfg5"] = bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_digest(args, host, L, n_rank, log)
     log(f"[bench] launch avg {avg_kern_s * 1e6:.1f} us -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.1%} of HBM peak)")
     return result
 
 
-def bench_pcie_digest(fn, host, L, n, width, dev, stream, log):
-    """Host-inclusive rate: inputs in pinned host memory, digests back to host, through the host
-    mode of the C ABI (one call = H2D + kernel + D2H, synchronous)."""
-    import numpy as np
-    import torch
-    pinned = torch.from_numpy(host).pin_memory()
-    out = np.empty((n, width), np.uint8)
-    hp = pinned.numpy()
-    fn(hp, L, n, out=out)                       # warm the workspace
-    reps = 5
+def host_rate(call, nbytes, reps=5):
+    """Mean wall time of `call` (after one untimed call that sizes the library's scratch)."""
+    call()
     t = time.perf_counter()
     for _ in range(reps):
-        fn(hp, L, n, out=out)
+        call()
     dt = (time.perf_counter() - t) / reps
-    return {"gib_s": round(host.nbytes / dt / 2**30, 2), "ms_per_batch": round(dt * 1e3, 3),
-            "note": "pinned host input -> H2D -> kernel -> D2H digests, synchronous host-mode call"}
+    return {"gib_s": round(nbytes / dt / 2**30, 2), "gb_s": round(nbytes / dt / 1e9, 2), "ms": round(dt * 1e3, 3)}
+
+
+def bench_pcie_digest(fn, host, L, n, width, log):
+    """Host-inclusive rate through the C ABI's host mode (input in host memory, digests back in host
+    memory, the call returns when they are there): pageable input (a plain numpy array, what a
+    receive loop's calloc'd buffers are) and page-locked input (torch pin_memory)."""
+    import numpy as np
+    import torch
+    out = np.empty((n, width), np.uint8)
+    pageable = host_rate(lambda: fn(host, L, n, out=out), host.nbytes)
+    pinned_t = torch.from_numpy(host).pin_memory()
+    hp = pinned_t.numpy()
+    pinned = host_rate(lambda: fn(hp, L, n, out=out), host.nbytes)
+    log(f"[bench] host-inclusive: pageable {pageable['gb_s']} GB/s, pinned {pinned['gb_s']} GB/s")
+    return {"gib_s": pageable["gib_s"], "ms_per_batch": pageable["ms"], "pageable": pageable, "pinned": pinned,
+            "note": "host-mode call: 16 MiB chunks copied H2D straight from the caller's memory, overlapped "
+                    "with the kernels; digests D2H at the end; gib_s = pageable input"}
+
+
+def bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log):
+    """BASELINE cfg5: 8 388 608 x 1500 B records sharded by contiguous ranges over 8 GPUs, 1 048 576
+    per GPU (no collective).  Every rank digests records [rank * 2^20, (rank + 1) *
+    2^20) of the cfg5 generator; at world 8 the job is exactly cfg5, at other N the same per-GPU
+    shard (weak scaling).  >= 1 s of warm-up, then K steps (>= 0.3 s) between barrier + synchronize,
+    max over ranks; 1.57 GB per
+    shard defeats the 256 MiB Infinity Cache by itself.  Both ends of each shard are checked
+    against the hashlib golden digests (tests/golden/digests.json configs["5"])."""
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+
+    L = workload.CONFIGS[5]["rec_len"]
+    n = workload.CONFIGS[5]["records"] // 8
+    r0 = rank * n
+    t = time.perf_counter()
+    host = workload.gen_records(workload.SEEDS[5], r0, n, L)
+    log(f"[bench] cfg5: generated {host.nbytes / 1e9:.2f} GB per GPU in {time.perf_counter() - t:.1f}s")
+    buf = torch.from_numpy(host).to(dev)
+    out = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    cfn = brb.lib().BRB_MD5BatchFixed
+    flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
+
+    def launch(k, s, j=0):
+        if cfn(buf.data_ptr(), L, n, out.data_ptr(), flags, s.cuda_stream) != 1:
+            raise RuntimeError(brb.lib().BRB_CryptoGPU_LastError().decode())
+
+    # the clock ramps down while the host-inclusive leg runs: warm up >= 1 s like the main steps
+    _, steps = warm_up(argparse.Namespace(warmup=None, steps=None), launch, [stream], torch, max_over_ranks)
+    wall, ev_s = timed_steps(launch, steps, [stream], barrier, max_over_ranks, torch)
+    got = out.cpu().numpy()
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        gold = json.load(f)["configs"]["5"]["digests"]
+    checked = 0
+    for e in gold:
+        if r0 <= e["r"] < r0 + n:
+            assert got[e["r"] - r0].tobytes().hex() == e["md5"], f"cfg5 digest mismatch at record {e['r']}"
+            checked += 1
+    for i in np.random.default_rng(rank + 5).integers(0, n, 16):
+        assert got[i].tobytes() == hashlib.md5(host[i * L:(i + 1) * L].tobytes()).digest()
+    launch_s = ev_s / steps
+    total = n * world
+    del buf, out
+    torch.cuda.empty_cache()
+    log(f"[bench] cfg5: {launch_s * 1e6:.1f} us per 1 Mi-record launch")
+    return {"workload": "cfg5: 8388608 x 1500 B MD5, record-sharded over 8 GPUs" if world == 8 else
+                        f"cfg5 shard shape: {n} x 1500 B MD5 per GPU x {world} GPU(s) (exactly cfg5 at --gpus 8)",
+            "records_total": total, "records_per_gpu": n, "steps": steps,
+            "value": round(total * L * steps / wall / 2**30, 2), "unit": "GiB/s",
+            "mrecords_per_s": round(total * steps / wall / 1e6, 3), "ms_per_step": round(wall / steps * 1e3, 4),
+            "launch_us_avg": round(launch_s * 1e6, 2),
+            "roofline_frac": round(n * L / launch_s / 1e9 / HBM_PEAK_GBS, 4),
+            "golden_checked_on_rank0": checked if rank == 0 else None,
+            "note": "per-GPU shard of 1 048 576 records; wall time max over ranks"}
 
 
 def cpu_baseline_digest(args, host, L, n, log):
@@ -350,7 +483,8 @@ def cpu_baseline_digest(args, host, L, n, log):
         res[th] = (n_s * L * reps / dt / 2**30, reps, n_s)
     gib, reps, n_s = res[threads]
     log(f"[bench] cpu baseline {gib:.2f} GiB/s on {threads} threads, {res[1][0]:.3f} GiB/s on 1")
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(gib, 3), "unit": "GiB/s", "kind": "port",
+            **core_counts(threads, res[1][0]),
             "sample": f"oracle/brb_oracle.c {args.op} over the same {n_s} x {L} B records, {reps} passes, "
                       f"{threads} pthreads (-O2 as libbrb_core/Makefile.linux:3)",
             "single_core_gib_s": round(res[1][0], 4)}
@@ -404,11 +538,13 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
                    "parallelism": f"record-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(4 * plain / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(4 * plain / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": (2 * load_traffic(args.pmc_summary, "cfg4_blowfish")
-                                 if load_traffic(args.pmc_summary, "cfg4_blowfish") else None),
+                     **traffic_fields(args.pmc_summary, "cfg4_blowfish", per_step=2),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": 4 * plain,
-                     "note": "algorithmic bytes = read + write of the plaintext in each direction"},
+                     "note": "algorithmic bytes = read + write of the plaintext in each direction",
+                     "compute": blowfish_compute(args.pmc_summary)},
     }
+    if world == 1 and not args.no_pcie:
+        result["pcie_inclusive"] = bench_pcie_blowfish(ctx, w, log)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         oc = oracle.bf_init(workload.CFG4_KEY)
         th = cpu_threads()
@@ -419,10 +555,112 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
             oracle.bf_ecb(oc, sample, decrypt=True, threads=th)
             reps += 1
         dt = time.perf_counter() - t0
+        one = sample[: len(sample) // 16].copy()
+        t1 = time.perf_counter()
+        oracle.bf_ecb(oc, one)
+        oracle.bf_ecb(oc, one, decrypt=True)
+        single = one.nbytes / (time.perf_counter() - t1) / 2**30
         result["cpu_baseline"] = {"value": round(sample.nbytes * reps / dt / 2**30, 3), "unit": "GiB/s",
-                                  "cores": th, "kind": "port",
-                                  "sample": f"oracle bf_ecb enc+dec over {sample.nbytes >> 20} MiB, {reps} passes"}
+                                  "kind": "port", **core_counts(th, single),
+                                  "single_core_gib_s": round(single, 4),
+                                  "sample": f"oracle bf_ecb enc+dec over {sample.nbytes >> 20} MiB, {reps} passes, "
+                                            f"{th} pthreads"}
     return result
+
+
+def blowfish_compute(path):
+    """roofline.compute for bf_rep_kernel: the LDS gathers bound it (four random 8-byte S-box reads
+    per F).  SQ_LDS_IDX_ACTIVE counts LDS-busy cycles summed over the 256 CUs (checked: 2.0 per
+    ds_read_b32 in the MD5 kernel, 3.0 per ds_read_b64 here = 2 + its one 2-way bank conflict), and
+    GRBM_GUI_ACTIVE / 8 is the dispatch's busy cycles per XCD (reliable on dispatches over 0.3 ms,
+    MI355X_MICROARCH.md "DVFS give-back"), so lds_busy_frac = (IDX_ACTIVE / 256) / (GUI_ACTIVE / 8)
+    with no clock assumption; valu_frac_peak = SQ_INSTS_VALU / 1024 SIMDs x 2 cycles over the same
+    cycles."""
+    _, det = load_pmc(path, "cfg4_blowfish")
+    if not det or "sq_lds_idx_active" not in det or "grbm_gui_active" not in det:
+        return None
+    cyc = det["grbm_gui_active"] / 8
+    return {"bound": "lds-gather", "dispatch_cycles": round(cyc),
+            "lds_busy_frac": round(det["sq_lds_idx_active"] / 256 / cyc, 4),
+            "lds_bank_conflict_frac": round(det.get("sq_lds_bank_conflict", 0) / 256 / cyc, 4),
+            "valu_frac_peak": round(det["sq_insts_valu"] / SIMDS * VALU_PEAK_CYC / cyc, 4),
+            "source": det.get("source")}
+
+
+def bench_pcie_blowfish(ctx, w, log):
+    """cfg4 host-inclusive: the 1 GiB of words in host memory, encrypted then decrypted in place by
+    two host-mode calls (every byte crosses PCIe four times per round trip); pageable and
+    page-locked.  Rate = plaintext bytes per round trip."""
+    import torch
+
+    import brb_framework_amd as brb
+    buf = w.copy()
+
+    def trip(b):
+        brb.blowfish_encrypt_batch(ctx, b)
+        brb.blowfish_decrypt_batch(ctx, b)
+
+    pageable = host_rate(lambda: trip(buf), w.nbytes, reps=3)
+    pin_t = torch.from_numpy(buf.view("int64")).pin_memory()
+    pb = pin_t.numpy().view("uint64")
+    pinned = host_rate(lambda: trip(pb), w.nbytes, reps=3)
+    assert (pb == w).all() and (buf == w).all(), "host-mode round trip did not restore the plaintext"
+    log(f"[bench] cfg4 host-inclusive: pageable {pageable['gib_s']} GiB/s, pinned {pinned['gib_s']} GiB/s")
+    return {"gib_s": pageable["gib_s"], "ms_per_round_trip": pageable["ms"], "pageable": pageable, "pinned": pinned,
+            "note": "two host-mode calls (encrypt, decrypt) over the 1 GiB in place: 16 MiB chunks, H2D on the calling "
+                    "thread and D2H on the device's worker thread overlap each other and the kernels"}
+
+
+# ------------------------------------------------------------------------------------------------
+def bench_cfg1(args):
+    """BASELINE cfg1 (plumbing, no GPU): one 1 048 576-byte buffer through the product's compat
+    BRB_MD5Init / BRB_MD5UpdateBig / BRB_MD5Final (md5.c:38-168) on one CPU thread, the digest
+    checked against the hashlib golden digest; the oracle's MD5 of the same buffer is timed beside
+    it as the CPU baseline."""
+    import ctypes
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+    import oracle
+
+    L = brb.lib()
+    cfg = workload.CONFIGS[1]
+    buf = workload.gen_records(workload.SEEDS[1], 0, 1, cfg["rec_len"]).tobytes()
+    with open(os.path.join(ROOT, "tests", "golden", "digests.json")) as f:
+        want = json.load(f)["configs"]["1"]["digests"][0]["md5"]
+    ctx = brb.BRB_MD5_CTX()
+
+    def compat():
+        L.BRB_MD5Init(ctypes.byref(ctx))
+        L.BRB_MD5UpdateBig(ctypes.byref(ctx), buf, len(buf))
+        L.BRB_MD5Final(ctypes.byref(ctx))
+
+    def timed(fn, seconds):
+        fn()
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            fn()
+            n += 1
+        return n, time.perf_counter() - t0
+
+    steps, dt = timed(compat, max(1.0, args.cpu_seconds / 2))
+    assert bytes(ctx.digest).hex() == want, "compat MD5 of the cfg1 buffer differs from the golden digest"
+    o_steps, o_dt = timed(lambda: oracle.md5(buf), max(1.0, args.cpu_seconds / 2))
+    assert oracle.md5(buf).hex() == want
+    rate = len(buf) * steps / dt / 2**30
+    o_rate = len(buf) * o_steps / o_dt / 2**30
+    return {"metric": "GiB/s of MD5 over one 1 MiB buffer through the compat BRB_MD5Init/UpdateBig/Final (cfg1, CPU)",
+            "value": round(rate, 3), "unit": "GiB/s", "n_gpus": 0, "steps": steps, "warmup": 1,
+            "ms_per_step": round(dt / steps * 1e3, 4), "higher_is_better": True, "scaling": "none",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic (SURVEY §8(d) generator, seed 0x5EED0001)",
+            "config": {"workload": cfg["name"], "op": "BRB_MD5Init + BRB_MD5UpdateBig + BRB_MD5Final (compat, host C)",
+                       "record_bytes": len(buf), "parallelism": "one CPU thread"},
+            "digest": bytes(ctx.digest).hex(), "golden_match": True,
+            "roofline": None,
+            "cpu_baseline": {"value": round(o_rate, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                             "sample": f"oracle/brb_oracle.c MD5 of the same 1 MiB buffer, {o_steps} passes"},
+            "note": "cfg1 is the reference's single-buffer CPU path (SURVEY §8(d)): a serial chain of 16 385 "
+                    "compressions, no GPU and no roofline"}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -502,7 +740,7 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                    "parallelism": f"connection-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(moved / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic(args.pmc_summary, f"f1_{args.op}"),
+                     **traffic_fields(args.pmc_summary, f"f1_{args.op}"),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
                      "note": "algorithmic bytes read+written per step; the bound in practice is the per-byte "
                              "RC4 dependency chain through LDS (DESIGN.md)"},
@@ -527,6 +765,7 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         dt = time.perf_counter() - t0
         assert hv.all()
         result["cpu_baseline"] = {"value": round(m * L * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": th,
+                                  "nproc_note": "threads = the lease's CPU share (see the digest line's cores_note)",
                                   "kind": "port",
                                   "sample": f"oracle frame+open of {m} connections x {L} B, {reps} passes, {th} pthreads"}
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")

@@ -32,17 +32,33 @@ using brb_api::set_err;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Bytes per chunk (BRB_HOST_CHUNK_BYTES overrides; read once).  16 MiB pieces copy at ≈ 53 GB/s
-// against 56.5 GB/s for one large copy, and a 98 MB cfg2 batch still gives six chunks to overlap.
+// Input bytes per chunk (read once; BRB_HOST_CHUNK_BYTES / BRB_HOST_DIGEST_CHUNK_BYTES override).
+// Every pageable chunk copy pays a fixed cost (8 MiB pieces copy at 52 GB/s, one 98 MB copy at
+// 56.5 GB/s), while only the first chunk's H2D and the last chunk's D2H go un-overlapped.
+// Blowfish returns as many bytes as it sends, so its ends are whole chunks: 16 MiB.  Digest
+// batches return 16-20 B per record, so their chunks can be larger: 32 MiB.
+size_t env_bytes(const char *name, size_t dflt)
+{
+    const char *e = getenv(name);
+    const long long x = e ? atoll(e) : 0;
+    return x >= 4096 ? size_t(x) : dflt;
+}
 size_t chunk_bytes()
 {
-    static const size_t v = [] {
-        const char *e = getenv("BRB_HOST_CHUNK_BYTES");
-        const long long x = e ? atoll(e) : 0;
-        return x >= 4096 ? size_t(x) : size_t(16) << 20;
-    }();
+    static const size_t v = env_bytes("BRB_HOST_CHUNK_BYTES", size_t(16) << 20);
     return v;
 }
+size_t digest_chunk_bytes()
+{
+    static const size_t v = env_bytes("BRB_HOST_DIGEST_CHUNK_BYTES", size_t(32) << 20);
+    return v;
+}
+
+// Posts "wait for `ev` on `s_out`, then copy [src, src + bytes) to host `dst`" to the device's D2H
+// worker: a D2H copy into pageable memory holds its thread until done, and on the worker it runs
+// while the calling thread goes on issuing H2D copies, so both PCIe directions are busy.
+class Pending;
+void post_d2h(int dev, Pending &pending, hipStream_t s_out, hipEvent_t ev, void *dst, const void *src, size_t bytes);
 
 // ---- persistent worker threads -------------------------------------------------------------------
 // One per (device, role): role 0 runs a device's share of an all-devices split, role 1 issues D2H
@@ -133,6 +149,22 @@ private:
     std::string err_;
 };
 
+void post_d2h(int dev, Pending &pending, hipStream_t s_out, hipEvent_t ev, void *dst, const void *src, size_t bytes)
+{
+    pending.add();
+    worker(dev, 1).post([=, &pending] {
+        hipError_t x;
+        int r = BRB_BATCH_OK;
+        std::string why;
+        if ((x = hipStreamWaitEvent(s_out, ev, 0)) != hipSuccess ||
+            (x = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s_out)) != hipSuccess) {
+            r = fail_hip("hipMemcpyAsync D2H", x);
+            why = brb_api::t_err;
+        }
+        pending.done(r, why);
+    });
+}
+
 // ---- per-thread, per-device streams and events ---------------------------------------------------
 constexpr int kEvents = 64;   // reused round-robin; a wait on a later record of the same event only
                               // waits longer (later chunks follow on the same stream)
@@ -196,9 +228,10 @@ int drain(Pipe *p, int rc)
     return rc;
 }
 
-// One device's share of a fixed-stride digest batch: H2D chunk by chunk on s_in, one kernel per
-// chunk on s_k once its bytes have landed, the digests back in one copy at the end (16-20 B per
-// record: ≈ 1 % of the input).
+// One device's share of a fixed-stride digest batch: H2D chunk by chunk on s_in (calling thread),
+// one kernel per chunk on s_k once its bytes have landed, and each chunk's digests back through the
+// device's D2H worker while later chunks are still going up (cfg3's 64-byte records return a
+// quarter of their bytes as digests).
 int digest_part(brb_host::FixedLauncher launch, size_t dig, const uint8_t *data, uint32_t L, uint64_t n,
                 uint8_t *digests)
 {
@@ -213,22 +246,30 @@ int digest_part(brb_host::FixedLauncher launch, size_t dig, const uint8_t *data,
     uint8_t *ws = static_cast<uint8_t *>(brb_api::workspace(off_out + dig * n, &e));
     if (!ws)
         return fail_hip("device workspace", e);
-    const uint64_t per = L ? std::max<uint64_t>(1, chunk_bytes() / L) : n;
+    const uint64_t per = L ? std::max<uint64_t>(1, digest_chunk_bytes() / L) : n;
+    Pending pending;
     int rc = BRB_BATCH_OK;
     uint64_t c = 0;
-    for (uint64_t i = 0; i < n && rc == BRB_BATCH_OK; i += per, c++) {
+    for (uint64_t i = 0; i < n && rc == BRB_BATCH_OK && !pending.failed(); i += per, c++) {
         const uint64_t m = std::min(per, n - i);
-        hipEvent_t ev = p->ev_in[c % kEvents];
+        hipEvent_t ev_in = p->ev_in[c % kEvents], ev_k = p->ev_k[c % kEvents];
         if (L && (e = hipMemcpyAsync(ws + i * L, data + i * L, m * L, hipMemcpyHostToDevice, p->s_in)) != hipSuccess)
             rc = fail_hip("hipMemcpyAsync H2D", e);
-        else if ((e = hipEventRecord(ev, p->s_in)) != hipSuccess || (e = hipStreamWaitEvent(p->s_k, ev, 0)) != hipSuccess)
+        else if ((e = hipEventRecord(ev_in, p->s_in)) != hipSuccess || (e = hipStreamWaitEvent(p->s_k, ev_in, 0)) != hipSuccess)
             rc = fail_hip("chunk event", e);
         else if ((e = launch(ws + i * L, L, m, ws + off_out + i * dig, p->s_k)) != hipSuccess)
             rc = fail_hip("kernel launch", e);
+        else if ((e = hipEventRecord(ev_k, p->s_k)) != hipSuccess)
+            rc = fail_hip("chunk event", e);
+        else
+            post_d2h(dev, pending, p->s_out, ev_k, digests + i * dig, ws + off_out + i * dig, dig * m);
     }
-    if (rc == BRB_BATCH_OK &&
-        (e = hipMemcpyAsync(digests, ws + off_out, dig * n, hipMemcpyDeviceToHost, p->s_k)) != hipSuccess)
-        rc = fail_hip("hipMemcpyAsync D2H", e);
+    std::string why;
+    const int rc_out = pending.wait(&why);
+    if (rc == BRB_BATCH_OK && rc_out != BRB_BATCH_OK) {
+        brb_api::t_err = why;
+        rc = rc_out;
+    }
     return drain(p, rc);
 }
 
@@ -253,7 +294,6 @@ int blowfish_part(const BRB_BLOWFISH_CTX *ctx, uint64_t *words, uint64_t nb, boo
     if ((e = hipMemcpyAsync(ws, ctx, sizeof(BRB_BLOWFISH_CTX), hipMemcpyHostToDevice, p->s_in)) != hipSuccess)
         return drain(p, fail_hip("hipMemcpyAsync H2D", e));
     const uint64_t per = std::max<uint64_t>(1, chunk_bytes() / 16);
-    Worker &out = worker(dev, 1);
     Pending pending;
     int rc = BRB_BATCH_OK;
     uint64_t c = 0;
@@ -268,23 +308,8 @@ int blowfish_part(const BRB_BLOWFISH_CTX *ctx, uint64_t *words, uint64_t nb, boo
             rc = fail_hip("kernel launch", e);
         else if ((e = hipEventRecord(ev_k, p->s_k)) != hipSuccess)
             rc = fail_hip("chunk event", e);
-        if (rc != BRB_BATCH_OK)
-            break;
-        pending.add();
-        hipStream_t s_out = p->s_out;
-        uint64_t *dst = words + 2 * i;
-        const uint64_t *src = dw + 2 * i;
-        out.post([=, &pending] {
-            hipError_t x;
-            int r = BRB_BATCH_OK;
-            std::string why;
-            if ((x = hipStreamWaitEvent(s_out, ev_k, 0)) != hipSuccess ||
-                (x = hipMemcpyAsync(dst, src, 16 * m, hipMemcpyDeviceToHost, s_out)) != hipSuccess) {
-                r = fail_hip("hipMemcpyAsync D2H", x);
-                why = brb_api::t_err;
-            }
-            pending.done(r, why);
-        });
+        else
+            post_d2h(dev, pending, p->s_out, ev_k, words + 2 * i, dw + 2 * i, 16 * m);
     }
     std::string why;
     const int rc_out = pending.wait(&why);

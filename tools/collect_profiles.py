@@ -55,7 +55,40 @@ def timed_region(trace_csv, pat, bench_json):
             "note": "bench_event_us_per_step includes the dependent-launch gap between back-to-back kernels"}
 
 
+COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT",
+            "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE", "SQ_WAVES")
+
+
+def counters(m):
+    """Per-dispatch means of the compute counters bench.py's roofline.compute reads (lower-case keys)."""
+    return {k.lower(): m[k] for k in COUNTERS if k in m}
+
+
+def backfill(tag):
+    """Adds the compute counters of the kept profiles/<tag>_pmc_<key>.txt summaries to
+    pmc_traffic.json (entries whose details predate them)."""
+    prof = os.path.join(ROOT, "profiles")
+    path = os.path.join(prof, "pmc_traffic.json")
+    traffic = json.load(open(path))
+    for key in [k for k in traffic if not k.endswith("_detail")]:
+        txt = os.path.join(prof, f"{tag}_pmc_{key}.txt")
+        if not os.path.exists(txt):
+            continue
+        m = {}
+        for ln in open(txt):
+            parts = ln.split()
+            if len(parts) == 2 and parts[0].isupper():
+                m[parts[0]] = float(parts[1])
+        traffic[key + "_detail"].update(counters(m))
+    with open(path, "w") as f:
+        json.dump(traffic, f, indent=1, sort_keys=True)
+        f.write("\n")
+
+
 def main():
+    if sys.argv[1] == "--backfill":
+        backfill(sys.argv[2])
+        return
     src, tag = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -96,7 +129,8 @@ def main():
             traffic[key + "_detail"] = {"fetch_bytes": int(fetch), "write_bytes": int(write),
                                         "source": f"profiles/{tag}_pmc_{key}.txt",
                                         "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024 per dispatch"
-                                                   + (f" x {per} dispatches per step" if per > 1 else "")}
+                                                   + (f" x {per} dispatches per step" if per > 1 else ""),
+                                        **counters(m)}
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1, sort_keys=True)
         f.write("\n")
