@@ -121,44 +121,42 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // logical granule by all lanes is conflict-free, ds_read_b32 of one logical dword 4-way at worst.
     auto swz = [](uint32_t row) { return (row >> 1) & 7; };
 
-    // ---- issue side: DMA lane j of instruction q stages granule j % 8 of row 8q + j / 8
-    uint32_t vq[8];
-    uint64_t gline = 0;                                        // first line of the issuing group
-    uint64_t gleft = 0;                                        // bytes from gline to end_line
-    // fastq: DMA q carries the instruction offset 1024 (q % 4), which lands in the LDS address as
-    // well, so one M0 write serves four DMAs; the voffset is lowered by the same amount.  Needs
-    // every voffset >= 3072 where q % 4 == 3: full groups and records of at least 160 bytes.
-    bool fastq = false;
-    auto dma_setup = [&](uint64_t g) {
+    // ---- issue side: DMA lane j of instruction q stages granule j % 8 of row 8q + j / 8 of the
+    // issuing group's next line.  One M0 write serves four DMAs: DMA q carries the instruction
+    // offset 1024 (q % 4), which lands in the LDS address as well, and its voffset is lowered by the
+    // same amount.  The descriptor base sits 4 KiB below the line (and num_records 4 KiB above the
+    // bytes left), so every voffset stays >= 1024 whatever the record length or group size: one DMA
+    // form for every group, no per-DMA M0 writes.
+    uint32_t vq[8], vqn[8];                                    // this group's, the next group's
+    // Descriptor of the next line to issue: base = that line - 4096, num_records = 4096 + bytes from
+    // the line to end_line, clamped to [0, 2^31 - 1].  Set once per group (dma_setup) and advanced
+    // by one line per issue with four scalar ops.  A group at least 2^31 - 4097 bytes from the end
+    // starts at 2^31 - 1 and stays above every voffset of its K + 1 lines (line_supported caps
+    // rec_len at 1 MiB: voffsets < 64 MiB + 8 KiB).
+    brb_dma::v4i rs, rsn;
+    // The next group's offsets and descriptor go to vqn / rsn (taken over once per group): written
+    // into vq / rs inside the loop, they made hipcc copy all eight offsets on every iteration.
+    auto dma_setup = [&](uint64_t g, uint32_t (&vq)[8], brb_dma::v4i &rs) {
         const uint64_t r0 = g * 64;
         const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
         const uint64_t a0 = dbase + r0 * rec_len;
-        gline = a0 & ~uint64_t(127);
-        gleft = end_line - gline;
+        const uint64_t gbase = (a0 & ~uint64_t(127)) - 4096;
+        const uint64_t gleft = end_line - gbase;
+        rs.x = __builtin_amdgcn_readfirstlane(int(uint32_t(gbase)));
+        rs.y = __builtin_amdgcn_readfirstlane(int(uint32_t(gbase >> 32) & 0xFFFF));
+        rs.z = __builtin_amdgcn_readfirstlane(int(gleft > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(gleft)));
+        rs.w = 0x00020000;
         const uint32_t o0 = uint32_t(a0) & 127;
-        fastq = last == 63 && rec_len >= 160;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const uint32_t row = 8 * q + (lane >> 3);
             const uint32_t rr = row < last ? row : last;
-            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row)) - (fastq ? 1024u * (q & 3) : 0u);
+            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row)) + 4096u - 1024u * (q & 3);
         }
     };
-    auto issue = [&](uint32_t slot, uint32_t k) {              // line k of the issuing group -> slot
-        // descriptor of line k: base gline + 128 k, num_records = bytes left to end_line clamped to
-        // [0, 2^31 - 1], in 32-bit scalar ops (gfx950 has no 64-bit ordered scalar compare)
-        const uint64_t base = gline + 128ull * k;
-        const int64_t left = int64_t(gleft) - int64_t(128u * k);
-        const int32_t lhi = int32_t(uint64_t(left) >> 32);
-        const uint32_t llo = uint32_t(left);
-        const uint32_t nrec = lhi < 0 ? 0u : (lhi > 0 || llo > 0x7FFFFFFFu) ? 0x7FFFFFFFu : llo;
-        brb_dma::v4i rs;
-        rs.x = int(uint32_t(base));
-        rs.y = int(uint32_t(base >> 32) & 0xFFFF);
-        rs.z = int(nrec);
-        rs.w = 0x00020000;
+    auto issue = [&](const uint32_t (&vq)[8], brb_dma::v4i &rs, uint32_t slot) {   // next line -> slot
         const uint32_t m = lds0 + slot * SLOT;
-        if (fastq) {
+        uint32_t keep;
 #define BRB_LINE_DMA8(POL)                                                                      \
     asm volatile("s_mov_b32 %0, m0\n\t"                                                          \
                  "s_mov_b32 m0, %10\n\t"                                                         \
@@ -178,32 +176,20 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
                  : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "v"(vq[4]), "v"(vq[5]), "v"(vq[6]), \
                    "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u)                                    \
                  : "memory")
-            uint32_t keep;
-            if constexpr (NT)
-                BRB_LINE_DMA8("nt ");
-            else
-                BRB_LINE_DMA8("");
+        if constexpr (NT)
+            BRB_LINE_DMA8("nt ");
+        else
+            BRB_LINE_DMA8("");
 #undef BRB_LINE_DMA8
-            return;
-        }
-#define BRB_LINE_DMA(POL)                                                  \
-    asm volatile("s_mov_b32 %0, m0\n\t"                                     \
-                 "s_mov_b32 m0, %3\n\t"                                     \
-                 "s_nop 0\n\t"                                              \
-                 "buffer_load_dwordx4 %1, %2, 0 offen " POL "lds\n\t"       \
-                 "s_mov_b32 m0, %0"                                          \
-                 : "=&s"(keep)                                               \
-                 : "v"(vq[q]), "s"(rs), "s"(m + 1024u * q)                   \
-                 : "memory")
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            uint32_t keep;
-            if constexpr (NT)
-                BRB_LINE_DMA("nt ");
-            else
-                BRB_LINE_DMA("");
-        }
-#undef BRB_LINE_DMA
+        // rs: the line after the issued one.  base += 128 with carry; num_records = max(nr - 128, 0)
+        // in scalar asm (hipcc lowers the saturating subtract to v_sub ... clamp, which moves the
+        // whole descriptor into VGPRs).
+        const uint64_t b = ((uint64_t(uint32_t(rs.y)) << 32) | uint32_t(rs.x)) + 128u;
+        rs.x = int(uint32_t(b));
+        rs.y = int(uint32_t(b >> 32));
+        int z = rs.z;
+        asm("s_sub_i32 %0, %0, 0x80\n\ts_max_i32 %0, %0, 0" : "+s"(z) : : "scc");
+        rs.z = z;
     };
 
     // ---- read side: window dword i of this lane -> LDS offset, for lines (k-1, k) in slots
@@ -221,8 +207,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             const uint32_t q = sh + i, qq = q & 31;
             const uint32_t a = row + ((((qq >> 2) ^ f) << 4) | ((qq & 3) << 2));
             ae[i] = q >= 32 ? a + SLOT : a;
-            ao[i] = q >= 32 ? a : a + SLOT;
-        }
+            ao[i] = ae[i] ^ SLOT;                              // slot 0 has bit 13 clear
+            asm volatile("" : "+v"(ao[i]));                    // keep both tables (hipcc would re-derive
+        }                                                      // ao with 32 XORs per iteration)
     };
 
     uint32_t w0[16], w1[16];
@@ -232,47 +219,60 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             w0[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
             w1[i] = *reinterpret_cast<const uint32_t *>(ring + ad[16 + i]);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // window in VGPRs before its slot is refilled
+        // window in VGPRs before its slot is refilled: lgkmcnt(0) (vmcnt 63, expcnt 7 = no wait).
+        // The builtin, not inline asm: the compiler's waitcnt pass then knows the reads are done and
+        // inserts no waits of its own before their uses.
+        __builtin_amdgcn_s_waitcnt(0xC07F);
     };
 
     BRB_LINE_PROBE_DECL
     BRB_LINE_PROBE(0);
-    dma_setup(g);
-    issue(0, 0);
-    issue(1, 1);
+    dma_setup(g, vq, rs);
+    issue(vq, rs, 0);
+    issue(vq, rs, 1);
     win_setup(g);
+    // One iteration k (1 <= k <= K): wait for line k, read the window (lines k-1, k), refill the
+    // slot of line k-1 with line k+1 (at k = K: start the next group's lines 0 and 1), hash blocks
+    // 2k-2 and 2k-1.  Unrolled by two so that each parity reads with its own address table; the
+    // loop thus holds four compress sites (the shared instruction cache holds them: unrolling the
+    // whole record did not fit).
+    auto step = [&](typename Alg::State &st, uint32_t k, const uint32_t (&ad)[32], uint32_t refill_slot) {
+        BRB_LINE_PROBE(1);
+        brb_dma::wait_vmcnt<0>();
+        read_window(ad);
+        BRB_LINE_PROBE(2);
+        if (k < K) {
+            issue(vq, rs, refill_slot);
+        } else if (gn < n_groups) {
+            dma_setup(gn, vqn, rsn);
+            issue(vqn, rsn, 0);
+            issue(vqn, rsn, 1);
+        }
+        const uint32_t b = 2 * k - 2;
+        if (b < nfull)
+            Alg::compress(st, w0);
+        if (b + 1 < nfull)
+            Alg::compress(st, w1);
+    };
     for (;;) {
         typename Alg::State st = Alg::iv();
-        // one iteration: wait for line k, read the window, refill the slot of line k-1 (or start
-        // the next group), hash blocks 2k-2 and 2k-1
-        // one compress site per block (the code must stay small: one wave per SIMD runs out of
-        // the shared instruction cache at once when the loop body is unrolled)
-        for (uint32_t k = 1; k <= K; k++) {
-            BRB_LINE_PROBE(1);
-            brb_dma::wait_vmcnt<0>();
-            if (k & 1)
-                read_window(ae);
-            else
-                read_window(ao);
-            BRB_LINE_PROBE(2);
-            if (k < K) {
-                issue((k + 1) & 1, k + 1);
-            } else if (gn < n_groups) {
-                dma_setup(gn);
-                issue(0, 0);
-                issue(1, 1);
-            }
-            const uint32_t b = 2 * k - 2;
-            if (b < nfull)
-                Alg::compress(st, w0);
-            if (b + 1 < nfull)
-                Alg::compress(st, w1);
+        for (uint32_t k = 1;; k += 2) {
+            step(st, k, ae, 0);                                // odd k: line k+1 goes to slot 0
+            if (k == K)
+                break;
+            step(st, k + 1, ao, 1);                            // even k: line k+1 goes to slot 1
+            if (k + 1 == K)
+                break;
         }
         line_finish<Alg, OUT_ALIGNED>(st, w0, w1, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
         g = gn;
         if (g >= n_groups)
             break;
         gn = DYN ? take() : g + wstride;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            vq[q] = vqn[q];
+        rs = rsn;
         win_setup(g);
     }
     BRB_LINE_PROBE(3);
@@ -281,8 +281,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
 // Line-aligned staging needs 4-byte record bases (the window shift is whole dwords).
 inline bool line_supported(const uint8_t *data, uint32_t rec_len)
 {
-    return rec_len > 64 && (rec_len & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0 &&
-           uint64_t(rec_len) * 64 + 256 < (uint64_t(1) << 31);
+    return rec_len > 64 && rec_len <= (1u << 20) && (rec_len & 3) == 0 && (reinterpret_cast<uintptr_t>(data) & 3) == 0;
 }
 
 inline unsigned device_cu_count()

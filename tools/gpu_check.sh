@@ -10,7 +10,7 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 && echo "smoke ok" &&
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && echo "bench ok" && cat "$OUT/bench.json" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --no-pcie > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" && echo "rocprof ok"
+    python3 bench.py --no-cpu-baseline --no-pcie --no-cfg5 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" && echo "rocprof ok"
 rc=$?
 tail -3 "$OUT/pytest_gpu.log"
 exit $rc

@@ -23,19 +23,22 @@ __device__ inline uint64_t pr_rt()
     return t;
 }
 #define BRB_LINE_PROBE 1
-#define BRB_LINE_PROBE_DECL uint64_t pr_c0 = 0, pr_r0 = 0, pr_tw = 0, pr_wait = 0;
+#define NP 6
+#define BRB_LINE_PROBE_DECL uint64_t pr_c0 = 0, pr_r0 = 0, pr_tw = 0, pr_wait = 0, pr_first = 0;
 #define BRB_LINE_PROBE(ev)                                                              \
     do {                                                                                \
         if ((ev) == 0) { pr_c0 = pr_clk(); pr_r0 = pr_rt(); }                           \
         if ((ev) == 1) pr_tw = pr_clk();                                                \
-        if ((ev) == 2) pr_wait += pr_clk() - pr_tw;                                     \
+        if ((ev) == 2) { pr_wait += pr_clk() - pr_tw; if (!pr_first) pr_first = pr_wait; } \
         if ((ev) == 3 && lane == 0) {                                                   \
-            uint64_t *o = g_probe + 5 * wave0;                                          \
+            uint64_t *o = g_probe + NP * wave0;                                         \
             o[0] = pr_c0; o[1] = pr_clk(); o[2] = pr_r0; o[3] = pr_rt(); o[4] = pr_wait;\
+            o[5] = pr_first;                                                            \
         }                                                                               \
     } while (0)
 
 #include "digest_dma.h"
+#include "line1_kernel.h"
 #include "md5_device.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -83,7 +86,7 @@ int main(int argc, char **argv)
     CK(hipMalloc(&o, n * 16));
     const uint64_t groups = (n + 63) / 64;
     uint64_t *pr;
-    CK(hipMalloc(&pr, 4096 * 5 * 8));
+    CK(hipMalloc(&pr, 4096 * NP * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
     struct V { const char *name; Kern k; };
     struct VG { const char *name; Kern k; int waves; };
@@ -91,21 +94,30 @@ int main(int argc, char **argv)
                  {"DMA64 dyn16", brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
                  {"DMA64 dyn8", brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
                  {"DMA64 only", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
-    VG vs[] = {{"LINE md5", brb_digest::digest_line_kernel<AlgLit, 4, true>, 4},
-              {"LINE md5 nt dyn8", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
-              {"LINE md5 nt dyn4", brb_digest::digest_line_kernel<AlgLit, 4, true, true, true>, 4},
-              {"LINE md5 nt", brb_digest::digest_line_kernel<AlgLit, 4, true, true>, 4},
-              {"LINE dma-only nt", brb_digest::digest_line_kernel<AlgNull, 4, true, true>, 4}};
+    // waves = -4: digest_line1_kernel (one group per wave, 4-wave workgroups, grid = groups / 4)
+    VG vs[] = {{"LINE md5 nt dyn8", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE1 ns3", brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
+              {"LINE1 ns2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
+              {"LINE1 ns2 u4", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
+              {"LINE1 ns3 spread", brb_digest::digest_line1_kernel<AlgLit, true, true, 3, true>, -4},
+              {"LINE1 ns2 spread", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, true>, -4},
+              {"LINE md5 nt dyn8 #2", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE1 ns3 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
+              {"LINE1 ns2 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
+              {"LINE1 ns2 u4 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
+              {"LINE1 dma-only ns3", brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
+              {"LINE dma-only nt dyn8", brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8}};
     int it = 0;
     const bool small = L <= 64;
     const int nv = small ? 4 : int(sizeof(vs) / sizeof(vs[0]));
     for (int vi = 0; vi < nv; vi++) {
         const VG &v = small ? vs64[vi] : vs[vi];
         // 4-wave workgroups: 2 per CU (4 for <= 64 B records); bigger (dyn): one per CU
-        const unsigned grid = v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, small ? 1024 : 512))
-                                           : unsigned(std::min<uint64_t>(groups, 256));
-        const uint64_t waves = std::min<uint64_t>(uint64_t(grid) * v.waves, groups);
-        const unsigned bs = 64 * v.waves;
+        const unsigned grid = v.waves == -4 ? unsigned((groups + 3) / 4)
+                              : v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, small ? 1024 : 512))
+                                             : unsigned(std::min<uint64_t>(groups, 256));
+        const uint64_t waves = std::min<uint64_t>(uint64_t(grid) * (v.waves < 0 ? 4 : v.waves), groups);
+        const unsigned bs = 64 * (v.waves < 0 ? 4 : v.waves);
         // warm up >= 0.5 s (clocks), then probe one launch out of a back-to-back burst
         hipEvent_t a, b;
         hipEventCreate(&a);
@@ -121,34 +133,35 @@ int main(int argc, char **argv)
             tot += ms;
         }
         for (int i = 0; i < 9; i++) hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
-        CK(hipMemsetAsync(pr, 0, 4096 * 5 * 8));
+        CK(hipMemsetAsync(pr, 0, 4096 * NP * 8));
         hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
         CK(hipDeviceSynchronize());
-        std::vector<uint64_t> all(4096 * 5), hp;
+        std::vector<uint64_t> all(4096 * NP), hp;
         CK(hipMemcpy(all.data(), pr, all.size() * 8, hipMemcpyDeviceToHost));
         std::vector<uint64_t> widx;
         for (uint64_t w = 0; w < 4096; w++)
-            if (all[5 * w + 1]) {
+            if (all[NP * w + 1]) {
                 widx.push_back(w);
-                hp.insert(hp.end(), &all[5 * w], &all[5 * w + 5]);
+                hp.insert(hp.end(), &all[NP * w], &all[NP * w + NP]);
             }
         (void)waves;
         const uint64_t nw = widx.size();
         uint64_t r0 = ~0ull, r1 = 0;
-        for (uint64_t w = 0; w < nw; w++) { r0 = std::min(r0, hp[5 * w + 2]); r1 = std::max(r1, hp[5 * w + 3]); }
-        std::vector<double> mhz, st, en, dur, wf;
+        for (uint64_t w = 0; w < nw; w++) { r0 = std::min(r0, hp[NP * w + 2]); r1 = std::max(r1, hp[NP * w + 3]); }
+        std::vector<double> mhz, st, en, dur, wf, fw;
         for (uint64_t w = 0; w < nw; w++) {
-            const uint64_t *q = &hp[5 * w];
+            const uint64_t *q = &hp[NP * w];
             const double rt = double(q[3] - q[2]) * 10.0;  // ns (100 MHz)
             mhz.push_back(double(q[1] - q[0]) / (rt * 1e-3));
             st.push_back(double(q[2] - r0) * 10.0 / 1000.0);
             en.push_back(double(q[3] - r0) * 10.0 / 1000.0);
             dur.push_back(rt / 1000.0);
             wf.push_back(double(q[4]) / double(q[1] - q[0]));
+            fw.push_back(double(q[5]) / (double(q[1] - q[0]) / dur.back()));   // us
         }
         {   // per-XCD (blockIdx % 8) mean end time, and a histogram of end times
             double sx[8] = {0}; int cx[8] = {0};
-            for (uint64_t w = 0; w < nw; w++) { sx[(widx[w] / v.waves) % 8] += en[w]; cx[(widx[w] / v.waves) % 8]++; }
+            for (uint64_t w = 0; w < nw; w++) { sx[(widx[w] / (v.waves < 0 ? 4 : v.waves)) % 8] += en[w]; cx[(widx[w] / (v.waves < 0 ? 4 : v.waves)) % 8]++; }
             printf("  waves %llu, per-XCD mean end us:", (unsigned long long)nw);
             for (int i = 0; i < 8; i++) printf(" %.1f", sx[i] / cx[i]);
             printf("\n  end pcts:");
@@ -161,6 +174,7 @@ int main(int argc, char **argv)
         printf("%-18s n=%llu L=%u  span %.2f us | clock MHz p50 %.0f | start us p0 %.2f p50 %.2f p100 %.2f | end us p0 %.2f p50 %.2f p100 %.2f | wave us p50 %.2f | wait frac p10 %.2f p50 %.2f p90 %.2f\n",
                v.name, (unsigned long long)n, L, double(r1 - r0) * 10.0 / 1000.0, pct(mhz, .5), pct(st, 0), pct(st, .5), pct(st, 1),
                pct(en, 0), pct(en, .5), pct(en, 1), pct(dur, .5), pct(wf, .1), pct(wf, .5), pct(wf, .9));
+        printf("  first line-pair wait us p10 %.2f p50 %.2f p90 %.2f p100 %.2f\n", pct(fw, .1), pct(fw, .5), pct(fw, .9), pct(fw, 1));
     }
     return 0;
 }
