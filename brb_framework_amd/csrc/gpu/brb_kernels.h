@@ -33,9 +33,10 @@ hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint
 // RC4 (rc4_kernels.hip): 264-byte BRB_RC4_State records, updated in place.  Stream i uses
 // states[sidx ? sidx[i] : i] (sidx: a connection table, the transform batcher's indirection).
 // ooffs: output offsets (nullptr = the input offsets, out mirrors in)
+// sector_out: write whole aligned 64-byte sectors (brb_io::SectorSnk) -- for outputs in host memory
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx = nullptr,
-                            const uint64_t *ooffs = nullptr);
+                            const uint64_t *ooffs = nullptr, bool sector_out = false);
 hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const uint64_t *offs, const uint32_t *lens,
                                const uint64_t *salts, uint8_t *frames, const uint64_t *foffs, uint64_t n,
                                hipStream_t s, const uint32_t *sidx = nullptr);

@@ -127,6 +127,121 @@ struct Snk {
     }
 };
 
+// Snk whose middle goes out as whole, aligned 64-byte memory sectors.  A stream starting at a
+// 4-byte offset inside a sector writes each sector in two pieces one 64-byte block apart (with
+// Snk::put16: four 16-byte stores at the stream's own alignment), and the L2 wrote most of them
+// back to HBM twice: the RC4 pass wrote 190.9 MB for 115.6 MB of output (profiles/
+// r01_pmc_f1_rc4.txt).  Here put16's memory-aligned dwords go into the lane's LDS row -- two
+// sectors, circular by absolute dword index -- and the sector the block completes is read back with
+// four ds_read_b128 and stored with four aligned 16-byte stores.  The stream's first partial sector
+// (shared with the previous stream) is stored dword by dword, and the dwords left in the row are
+// stored dword by dword before the byte-exact tail (drain).  Rows are 144 bytes apart (36 banks):
+// lanes writing the same row position meet at most 4-way.
+struct SectorSnk {
+    static constexpr uint32_t kRowBytes = 144;
+    Snk s;                     // the byte-exact ends and the current position
+    uint32_t ta[16], tb[16];   // LDS addresses of row positions (u + i) & 31 for (u & 16) = 0 / 16
+    uint32_t rowb;             // LDS address of the row
+    uint32_t pend;             // dwords in the row not yet stored (0..15), ending at the position u
+    bool whole;                // the pending dwords start at a sector boundary (not the stream's first)
+
+    // `row` = this lane's 144-byte LDS row (16-byte aligned), as an LDS address
+    BRB_DEV void init(uint8_t *a, uint64_t n, uint32_t row)
+    {
+        s.init(a, n);
+        rowb = row;
+        pend = 0;
+        whole = false;
+        const uint32_t d = uint32_t(reinterpret_cast<uintptr_t>(s.p) >> 2) & 15;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++) {
+            ta[i] = row + 4 * ((d + i) & 31);
+            tb[i] = row + 4 * ((d + 16 + i) & 31);
+        }
+    }
+
+    static BRB_DEV uint32_t lds_ld(uint32_t a) { return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(a); }
+    static BRB_DEV void lds_st(uint32_t a, uint32_t v) { *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(a) = v; }
+
+    // stores the `pend` dwords before the current position that are only in the row
+    BRB_DEV void drain()
+    {
+        const uint32_t u = uint32_t(reinterpret_cast<uintptr_t>(s.p) >> 2);
+#pragma unroll
+        for (uint32_t i = 1; i <= 15; i++)
+            if (i <= pend)
+                stg(s.p - i, lds_ld(rowb + 4 * ((u - i) & 31)));
+        pend = 0;
+    }
+
+    BRB_DEV void put(uint32_t v)
+    {
+        if (pend)
+            drain();
+        s.put(v);
+    }
+
+    BRB_DEV void flush()
+    {
+        if (pend)
+            drain();
+        s.flush();
+    }
+
+    BRB_DEV void put16(const uint32_t (&v)[16])
+    {
+        if (s.first || s.rem < 64) {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                put(v[k]);
+            return;
+        }
+        const uint32_t o = s.o;
+        const uint32_t sel = 0x07060504u - 0x01010101u * o;    // as Snk::put16
+        uint32_t w[16];
+        uint32_t prev = o ? s.carry << (8 * (4 - o)) : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            w[k] = __builtin_amdgcn_perm(v[k], prev, sel);
+            prev = v[k];
+        }
+        const uint32_t u = uint32_t(reinterpret_cast<uintptr_t>(s.p) >> 2);   // absolute dword index
+        if (u & 16) {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                lds_st(tb[i], w[i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                lds_st(ta[i], w[i]);
+        }
+        // the sector holding dword u is complete: its dwords before u came with the previous block
+        // (pend of them; none of a stream's first sector went through the row)
+        const uint32_t d = u & 15;
+        const uint32_t half = rowb + 64 * ((u >> 4) & 1);
+        uint32_t *sec = s.p - d;
+        if (whole || d == 0) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                const v4u x = *reinterpret_cast<const __attribute__((address_space(3))) v4u *>(half + 16 * q);
+                st16_a4(reinterpret_cast<uint8_t *>(sec + 4 * q), x.x, x.y, x.z, x.w);
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++)
+                if (i >= d)
+                    stg(sec + i, lds_ld(half + 4 * i));
+        }
+        whole = true;
+        pend = d;
+        s.p += 16;
+        s.carry = o ? (v[15] >> (32 - 8 * o)) : 0u;
+        s.carry_n = o;
+        s.rem -= 64;
+    }
+};
+
 // 64-byte blocks of a byte range at any address, the next block always in flight: a lane that
 // consumes one block per few thousand cycles (RC4, a digest) never waits on HBM latency.  Block b
 // is 16 little-endian chunks, chunk i = range bytes 64 b + 4 i .. + 3; bytes past the range are 0.

@@ -10,6 +10,9 @@
 //                      last                                (ev_kq_aio_transform.c:212-230, 281-283)
 //   rc4md5_open_kernel READ side + EvAIOReqTransform_RC4_MD5_DataValidate: one pass decrypts the
 //                      frame and feeds the decrypted payload to MD5       (:270-279, :158-184)
+#include <cstdlib>
+#include <type_traits>
+
 #include "brb_kernels.h"
 #include "rc4_device.h"
 
@@ -69,6 +72,13 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
     decrypt_block(c, snk, g, F, b, pt);
 }
 
+// SECTOR: outputs through brb_io::SectorSnk (whole aligned 64-byte sectors) instead of Snk.
+// Measured (tools/gpu_rc4_sector.sh, 65 536 x 1500 B, two interleaved rounds): HBM outputs 123.0 ->
+// 128.3 us per pass (the sink's LDS row and address selects add ~50 VALU per block to ~1 100 for the
+// keystream) for 190.9 -> 152.8 MB written; zero-copy batcher rounds (outputs into page-locked host
+// memory over PCIe) 1.87 -> 1.81 ms pipelined, 2.50 -> 2.54 ms one round at a time.  So HBM outputs
+// keep Snk and the zero-copy batcher uses SectorSnk.
+template <bool SECTOR>
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
                                                           const uint32_t *__restrict__ lens, uint64_t n,
@@ -77,6 +87,7 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
 {
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
     __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t rows[SECTOR ? kWave * brb_io::SectorSnk::kRowBytes : 16];
     const uint64_t s = uint64_t(blockIdx.x) * kWave + threadIdx.x;
     const bool live = s < n;                     // lanes past n only help with the block loads
     Gen g;
@@ -92,9 +103,12 @@ __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ 
         ooff = ooffs ? ooffs[s] : off;
     }
     brb_io::BlockSrcW src;
-    Snk snk;
+    std::conditional_t<SECTOR, brb_io::SectorSnk, Snk> snk;
     src.init(in + off, len, xch + (threadIdx.x >> 6) * kXchBytes);
-    snk.init(out + ooff, len);
+    if constexpr (SECTOR)
+        snk.init(out + ooff, len, uint32_t(reinterpret_cast<uintptr_t>(rows)) + threadIdx.x * brb_io::SectorSnk::kRowBytes);
+    else
+        snk.init(out + ooff, len);
     const uint64_t nblk = (len + 63) >> 6;
     const uint32_t nloop = wave_max(uint32_t(nblk));
     uint32_t c[16];
@@ -305,11 +319,21 @@ namespace brb {
 
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx,
-                            const uint64_t *ooffs)
+                            const uint64_t *ooffs, bool sector_out)
 {
     if (n == 0)
         return hipSuccess;
-    rc4_crypt_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
+    // BRB_TEST_RC4_SECTOR=0/1 forces the sink for A/B measurements (tools/gpu_rc4_sector.sh)
+    static const int force = [] {
+        const char *e = getenv("BRB_TEST_RC4_SECTOR");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (force >= 0)
+        sector_out = force == 1;
+    if (sector_out)
+        rc4_crypt_kernel<true><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
+    else
+        rc4_crypt_kernel<false><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
     return hipGetLastError();
 }
 

@@ -515,7 +515,7 @@ static int enqueue_round(BRB_TransformBatcher *b, Round &R, bool *started)
         if (b->zc) {
             // inputs read in place over PCIe, outputs written into the page-locked output arena
             if (b->algo == BRB_CRYPTO_FUNC_RC4) {
-                e = brb::launch_rc4_crypt(b->d_states, zbase, zbase, offs, lens, g.count, s, sidx, ooffs);
+                e = brb::launch_rc4_crypt(b->d_states, zbase, zbase, offs, lens, g.count, s, sidx, ooffs, true);
             } else if (g.op == BRB_CRYPTO_OP_WRITE) {
                 e = brb::launch_rc4md5_frame(b->d_states, zbase, offs, lens, salts, zbase, ooffs, g.count, s, sidx);
             } else {

@@ -97,6 +97,7 @@ int main(int argc, char **argv)
     const int zc = argc > 5 ? atoi(argv[5]) : 0;
     const int pipelined = argc > 6 ? atoi(argv[6]) : 0;
     const uint32_t T = argc > 7 && atoi(argv[7]) > 0 ? (uint32_t)atoi(argv[7]) : 1;
+    const int algo = argc > 8 && atoi(argv[8]) == 1 ? BRB_CRYPTO_FUNC_RC4 : BRB_CRYPTO_FUNC_RC4_MD5;
     /* every round's frames are built before timing (each depends on the peer's RC4 state) */
     const int NR = W + R;
     const uint32_t F = L + BRB_RC4MD5_HEADER;
@@ -115,7 +116,7 @@ int main(int argc, char **argv)
         return 1;
     }
     BRB_TransformBatcher *b = BRB_TransformBatcherCreate(C, (uint64_t)C * (L + F) * 102 / 100 + (uint64_t)T * (256 << 10) + 4096,
-                                                         BRB_CRYPTO_FUNC_RC4_MD5 | (zc ? BRB_BATCHER_ZERO_COPY : 0) |
+                                                         algo | (zc ? BRB_BATCHER_ZERO_COPY : 0) |
                                                              (pipelined ? BRB_BATCHER_PIPELINED : 0));
     if (!b) {
         printf("{\"error\": \"%s\"}\n", BRB_CryptoGPU_LastError());
