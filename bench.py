@@ -569,8 +569,9 @@ def bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks,
 
 
 def blowfish_compute(path):
-    """roofline.compute for bf_rep_kernel: the LDS gathers bound it (four random 8-byte S-box reads
-    per F).  SQ_LDS_IDX_ACTIVE counts LDS-busy cycles summed over the 256 CUs (checked: 2.0 per
+    """roofline.compute for bf_rep_kernel: SIMD instruction issue bounds it (every SIMD issues on
+    ~100 % of the cycles at ~4 cycles per instruction: 11 VALU + 4 LDS gathers per F), the LDS gathers
+    come second.  SQ_LDS_IDX_ACTIVE counts LDS-busy cycles summed over the 256 CUs (checked: 2.0 per
     ds_read_b32 in the MD5 kernel, 3.0 per ds_read_b64 here = 2 + its one 2-way bank conflict), and
     GRBM_GUI_ACTIVE / 8 is the dispatch's busy cycles per XCD (reliable on dispatches over 0.3 ms,
     MI355X_MICROARCH.md "DVFS give-back"), so lds_busy_frac = (IDX_ACTIVE / 256) / (GUI_ACTIVE / 8)
@@ -580,11 +581,18 @@ def blowfish_compute(path):
     if not det or "sq_lds_idx_active" not in det or "grbm_gui_active" not in det:
         return None
     cyc = det["grbm_gui_active"] / 8
-    return {"bound": "lds-gather", "dispatch_cycles": round(cyc),
-            "lds_busy_frac": round(det["sq_lds_idx_active"] / 256 / cyc, 4),
-            "lds_bank_conflict_frac": round(det.get("sq_lds_bank_conflict", 0) / 256 / cyc, 4),
-            "valu_frac_peak": round(det["sq_insts_valu"] / SIMDS * VALU_PEAK_CYC / cyc, 4),
-            "source": det.get("source")}
+    out = {"bound": "simd-issue, then lds-gather", "dispatch_cycles": round(cyc),
+           "lds_busy_frac": round(det["sq_lds_idx_active"] / 256 / cyc, 4),
+           "lds_bank_conflict_frac": round(det.get("sq_lds_bank_conflict", 0) / 256 / cyc, 4),
+           "valu_frac_peak": round(det["sq_insts_valu"] / SIMDS * VALU_PEAK_CYC / cyc, 4),
+           "source": det.get("source")}
+    if "sq_active_inst_any" in det:
+        # SQ_ACTIVE_INST_ANY: quad-cycles in which a wave issued, summed over waves; x 4 / 1024 SIMDs
+        # = the cycles each SIMD spent issuing (4 waves per SIMD here, at most one issuing at a time)
+        out["issue_busy_frac"] = round(det["sq_active_inst_any"] * 4 / SIMDS / cyc, 4)
+        insts = det["sq_insts_valu"] + det.get("sq_insts_lds", 0) + det.get("sq_insts_salu", 0)
+        out["cycles_per_issued_inst"] = round(det["sq_active_inst_any"] * 4 / insts, 2)
+    return out
 
 
 def bench_pcie_blowfish(ctx, w, log):

@@ -1,9 +1,14 @@
-"""N > 1 path on CPU: record sharding with world_size 2 over gloo.
+"""N > 1 path: record sharding with world_size 2 over gloo.
 
-Each rank takes a contiguous record range (workload.shard), digests it (here with the CPU oracle
-standing in for the device call, which needs a GPU), and the shards are gathered.  The gathered
-digests must equal the unsharded batch; the timing reduction is the bench's max-over-ranks.
-No collective touches record data in the product path -- the all_gather here is the test's check.
+Each rank takes a contiguous record range (workload.shard, the same rule as the library's
+BRB_BATCH_ALL_DEVICES split), digests it with the PRODUCT library, and the shards are gathered.  The
+gathered digests must equal the oracle's digests of the unsharded batch; the timing reduction is the
+bench's max-over-ranks.  No collective touches record data in the product path -- the all_gather here
+is the test's check.
+  * mode "compat" (CPU, runs here): every record through the library's compat surface
+    (BRB_MD5Init / BRB_MD5Update / BRB_MD5Final, libbrb_crypto_gpu.so host code);
+  * mode "gpu" (-m gpu): each rank's shard through BRB_MD5BatchFixed in device mode on its GPU
+    (rank % visible devices: both ranks share the card on a one-GPU box).
 """
 import os
 import socket
@@ -25,14 +30,32 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, L, q):
-    import oracle
+def _digest_shard(mode, rank, data, L, m):
+    import ctypes
+
+    import brb_framework_amd as brb
+    if mode == "gpu":
+        dev = torch.device("cuda", rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        return brb.md5_batch_fixed(torch.from_numpy(data).to(dev), L, m).cpu().numpy()
+    L_ = brb.lib()
+    out = np.empty((m, 16), np.uint8)
+    for i in range(m):
+        c = brb.BRB_MD5_CTX()
+        L_.BRB_MD5Init(ctypes.byref(c))
+        L_.BRB_MD5Update(ctypes.byref(c), data[i * L:(i + 1) * L].tobytes(), L)
+        L_.BRB_MD5Final(ctypes.byref(c))
+        out[i] = np.frombuffer(bytes(c.digest), np.uint8)
+    return out
+
+
+def _worker(rank, world, port, n, L, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         r0, r1 = workload.shard(n, rank, world)
         data = workload.gen_records(workload.SEEDS[5], r0, r1 - r0, L)
-        dig = oracle.md5_batch_fixed(data, L, r1 - r0)
+        dig = _digest_shard(mode, rank, data, L, r1 - r0)
         # variable-size shards: gather through a padded buffer + the true sizes
         size = torch.tensor([r1 - r0])
         sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
@@ -52,14 +75,13 @@ def _worker(rank, world, port, n, L, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [1000, 1025])
-def test_sharded_digests_equal_unsharded(n):
+def _run_sharded(n, mode):
     import oracle
     L = 1500
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, L, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, L, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     full, tmax = q.get(timeout=120)
@@ -69,6 +91,17 @@ def test_sharded_digests_equal_unsharded(n):
     want = oracle.md5_batch_fixed(workload.gen_records(workload.SEEDS[5], 0, n, L), L, n)
     assert np.array_equal(full, want)
     assert tmax == 2.0
+
+
+@pytest.mark.parametrize("n", [1000, 1025])
+def test_sharded_compat_digests_equal_unsharded(n):
+    _run_sharded(n, "compat")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [70_001])
+def test_sharded_gpu_digests_equal_unsharded(n):
+    _run_sharded(n, "gpu")
 
 
 def test_shard_ranges_partition():

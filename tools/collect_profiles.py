@@ -56,7 +56,8 @@ def timed_region(trace_csv, pat, bench_json):
 
 
 COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT",
-            "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE", "SQ_WAVES")
+            "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY",
+            "GRBM_GUI_ACTIVE", "SQ_WAVES")
 
 
 def counters(m):
@@ -110,6 +111,7 @@ def main():
         traffic = {}
     # (pass directory, key, kernel filter, dispatches per bench step)
     for sub, key, pat, per in (("pmc2", "cfg2_md5", "Md5Alg", 1), ("pmc2s", "cfg2_sha1", "Sha1Alg", 1),
+                               ("pmc3", "cfg3_md5", "Md5Alg", 1),
                                ("pmc4", "cfg4_blowfish", "bf_rep_kernel", 1),
                                ("pmc_rc4", "f1_rc4", "rc4_crypt_kernel", 1),
                                ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2)):

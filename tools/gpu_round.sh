@@ -15,6 +15,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --outp
     python3 bench.py --config 4 --no-cpu-baseline > "$OUT/bench4_prof.json" 2> "$OUT/bench4_prof.err" && echo "rocprof4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc2" --config 2 > /dev/null && echo "pmc2 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc2s" --config 2 --op sha1 > /dev/null && echo "pmc2s ok" &&
+bash tools/gpu_pmc.sh "${1:-round}/pmc3" --config 3 > /dev/null && echo "pmc3 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc4" --config 4 > /dev/null && echo "pmc4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4" --op rc4 > /dev/null && echo "pmc rc4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4md5" --op rc4md5 > /dev/null && echo "pmc rc4md5 ok"
