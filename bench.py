@@ -155,12 +155,20 @@ def main():
     import brb_framework_amd as brb
     from brb_framework_amd import workload
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; RCCL ("nccl") for the barrier and the max-over-ranks.  Only when ranks
+    # outnumber the visible GPUs (a rehearsal of --gpus 2 on a one-GPU box) do they share a card and
+    # use gloo (RCCL refuses two ranks on one device).
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local_rank % ndev)
+    dev = torch.device("cuda", local_rank % ndev)
     dist = None
+    backend = "nccl" if world <= ndev else "gloo"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     if not brb.gpu_available():
         raise SystemExit("libbrb_crypto_gpu: " + brb.lib().BRB_CryptoGPU_LastError().decode())
 
@@ -171,7 +179,7 @@ def main():
     def max_over_ranks(x: float) -> float:
         if dist is None:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -350,7 +358,8 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "dtype": "u32",
         "data": "synthetic (SURVEY §8(d) splitmix64 generator, HBM-resident, L3-defeating rotation of "
                 f"{n_rot} copies)",
-        "config": {"workload": cfg["name"] + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else ""),
+        "config": {"workload": cfg["name"] + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else "")
+                   + (f"; the same batch on each of {world} GPUs" if world > 1 and cfg_id != 5 else ""),
                    "op": f"{'BRB_MD5BatchFixed' if args.op == 'md5' else 'BrbSha1_BatchFixed'} (device mode)",
                    "records_per_gpu": n_rank, "record_bytes": L, "global_records": n_global,
                    "parallelism": f"record-shard x{world}, no collective"},
@@ -403,8 +412,8 @@ def bench_pcie_digest(fn, host, L, n, width, log):
     pinned = host_rate(lambda: fn(hp, L, n, out=out), host.nbytes)
     log(f"[bench] host-inclusive: pageable {pageable['gb_s']} GB/s, pinned {pinned['gb_s']} GB/s")
     return {"gib_s": pageable["gib_s"], "ms_per_batch": pageable["ms"], "pageable": pageable, "pinned": pinned,
-            "note": "host-mode call: 16 MiB chunks copied H2D straight from the caller's memory, overlapped "
-                    "with the kernels; digests D2H at the end; gib_s = pageable input"}
+            "note": "host-mode call: 32 MiB chunks of whole records copied H2D straight from the caller's memory, overlapped "
+                    "with the kernels, digests D2H per chunk; gib_s = pageable input"}
 
 
 def bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log):

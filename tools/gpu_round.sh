@@ -9,6 +9,8 @@ mkdir -p "$OUT"
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 && echo "pytest ok" &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 && echo "smoke ok" &&
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && echo "bench ok" && cat "$OUT/bench.json" &&
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
+    bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --no-pcie > "$OUT/bench_n2.json" 2> "$OUT/bench_n2.err" && echo "bench n2 ok" && cat "$OUT/bench_n2.json" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --no-cpu-baseline --no-pcie --no-cfg5 > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" && echo "rocprof ok" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- \
