@@ -35,41 +35,42 @@
 namespace brb_digest {
 
 // Padding, digest and store of one group: the record's tail block (if any) is window half
-// nfull - (2K - 2) of the last iteration; bytes past the record are masked (md5.c:134-168).
+// nfull - (2K - 2) of the last iteration; bytes past the record are masked (md5.c:134-168).  The
+// tail's per-dword keep masks and 0x80 marker (tm, tp) depend only on rec_len: they are built once
+// per wave (tail_masks) while the first lines are in flight, so a group pays 16 v_and_or here.
 template <class Alg, bool OUT_ALIGNED>
-BRB_DEV void line_finish(typename Alg::State &st, const uint32_t (&w0)[16], const uint32_t (&w1)[16], uint32_t t,
-                         uint32_t nfull, uint32_t K, uint32_t rec_len, uint8_t *out, uint64_t r, uint64_t n_rec)
+BRB_DEV void line_finish(typename Alg::State &st, const uint32_t (&w0)[16], const uint32_t (&w1)[16],
+                         const uint32_t (&tm)[16], const uint32_t (&tp)[16], uint32_t t, uint32_t nfull, uint32_t K,
+                         uint32_t rec_len, uint8_t *out, uint64_t r, uint64_t n_rec)
 {
-    uint32_t tt = t;
-    asm volatile("" : "+s"(tt));                               // keep the tail math here, once per group
-    if (tt == 0) {
+    if (t == 0) {
         Alg::pad_only(st, rec_len);                            // the padding block is a constant
         if (r < n_rec)
             Alg::template store<OUT_ALIGNED>(out, r, st);
         return;
     }
     uint32_t w[16];
-    if (nfull + 2 - 2 * K) {
+    const bool second = nfull + 2 - 2 * K;                     // uniform: which half holds the tail
 #pragma unroll
-        for (int i = 0; i < 16; i++)
-            w[i] = w1[i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            w[i] = w0[i];
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < 16; i++) {
-        const uint32_t o = 4 * i;
-        const uint32_t keep = tt > o ? (tt - o < 4 ? tt - o : 4) : 0;
-        uint32_t v = w[i] & uint32_t((uint64_t(1) << (8 * keep)) - 1);
-        if (tt >= o && tt < o + 4)
-            v |= 0x80u << (8 * (tt - o));
-        w[i] = v;
-    }
+    for (int i = 0; i < 16; i++)
+        w[i] = ((second ? w1[i] : w0[i]) & tm[i]) | tp[i];
     Alg::finish(st, w, t, rec_len);
     if (r < n_rec)
         Alg::template store<OUT_ALIGNED>(out, r, st);
+}
+
+// Keep mask and marker of tail dword i for a tail of t bytes (0 < t < 64): bytes below t kept,
+// 0x80 at byte t, zeros after.  Kept in VGPRs (asm barrier) so that no group recomputes them.
+BRB_DEV void tail_masks(uint32_t t, uint32_t (&tm)[16], uint32_t (&tp)[16])
+{
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+        const uint32_t o = 4 * i;
+        const uint32_t keep = t > o ? (t - o < 4 ? t - o : 4) : 0;
+        tm[i] = uint32_t((uint64_t(1) << (8 * keep)) - 1);
+        tp[i] = t >= o && t < o + 4 ? 0x80u << (8 * (t - o)) : 0u;
+        asm volatile("" : "+v"(tm[i]), "+v"(tp[i]));
+    }
 }
 
 // Group assignment.  Static (DYN = false): wave w of the grid takes groups w, w + W_total, ...
@@ -108,8 +109,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     uint64_t g = DYN ? uint64_t(blockIdx.x) + uint64_t(wv) * gridDim.x : wave0;
     if (g >= n_groups)
         return;
-    uint64_t gn = DYN ? take() : g + wstride;                  // the group after g
-
     const uint32_t my_off = wv * 2 * SLOT;                     // slot 0; slot 1 = my_off + SLOT (bit 13 clear)
     const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + my_off;
     const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
@@ -146,12 +145,17 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         rs.y = __builtin_amdgcn_readfirstlane(int(uint32_t(gbase >> 32) & 0xFFFF));
         rs.z = __builtin_amdgcn_readfirstlane(int(gleft > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(gleft)));
         rs.w = 0x00020000;
+        // DMA q stages row 8q + lane/8 (rows past `last` re-stage row `last`): its line offset is
+        // min(row, last) * rec_len = min(row * rec_len, last * rec_len), one multiply per group; and
+        // swz(8q + l3) = (l3 >> 1) ^ 4(q & 1), so the granule swizzle takes two values.  4 VALU per DMA.
         const uint32_t o0 = uint32_t(a0) & 127;
+        const uint32_t l3 = lane >> 3;
+        const uint32_t base = o0 + l3 * rec_len, cap = o0 + last * rec_len;
+        const uint32_t g0 = 16u * ((lane & 7) ^ (l3 >> 1));
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const uint32_t row = 8 * q + (lane >> 3);
-            const uint32_t rr = row < last ? row : last;
-            vq[q] = ((o0 + rr * rec_len) & ~127u) + 16 * ((lane & 7) ^ swz(row)) + 4096u - 1024u * (q & 3);
+            const uint32_t x = base + 8u * q * rec_len;
+            vq[q] = (((x < cap ? x : cap) & ~127u) | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
         }
     };
     auto issue = [&](const uint32_t (&vq)[8], brb_dma::v4i &rs, uint32_t slot) {   // next line -> slot
@@ -200,13 +204,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
         const uint32_t o0 = uint32_t(dbase + r0 * rec_len) & 127;
         const uint32_t rr = lane < last ? lane : last;
-        const uint32_t sh = ((o0 + rr * rec_len) & 127) >> 2;
-        const uint32_t f = swz(lane), row = my_off + lane * 128;
+        const uint32_t sh4 = (o0 + rr * rec_len) & 127;        // 4 x the record's dword shift
+        // Stream dword q = sh + i sits at row byte ((4q mod 128) ^ 16 swz) of slot q >= 32: with
+        // fr = row base | 16 swz (disjoint bits), one xor, one or and the slot bit.
+        const uint32_t fr = (my_off + lane * 128) | (swz(lane) << 4);
 #pragma unroll
         for (uint32_t i = 0; i < 32; i++) {
-            const uint32_t q = sh + i, qq = q & 31;
-            const uint32_t a = row + ((((qq >> 2) ^ f) << 4) | ((qq & 3) << 2));
-            ae[i] = q >= 32 ? a + SLOT : a;
+            const uint32_t q4 = sh4 + 4 * i;                   // < 256
+            ae[i] = ((q4 & 124u) ^ fr) | ((q4 & 128u) << 6);   // SLOT = 128 << 6
             ao[i] = ae[i] ^ SLOT;                              // slot 0 has bit 13 clear
             asm volatile("" : "+v"(ao[i]));                    // keep both tables (hipcc would re-derive
         }                                                      // ao with 32 XORs per iteration)
@@ -230,7 +235,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     dma_setup(g, vq, rs);
     issue(vq, rs, 0);
     issue(vq, rs, 1);
+    // Everything else of the prologue runs while the first two lines are in flight: without the
+    // barrier hipcc hoisted the window tables (~300 VALU) above the first DMA.
+    __builtin_amdgcn_sched_barrier(0);
+    uint64_t gn = DYN ? take() : g + wstride;                  // the group after g
     win_setup(g);
+    uint32_t tm[16], tp[16];
+    tail_masks(t, tm, tp);
     // One iteration k (1 <= k <= K): wait for line k, read the window (lines k-1, k), refill the
     // slot of line k-1 with line k+1 (at k = K: start the next group's lines 0 and 1), hash blocks
     // 2k-2 and 2k-1.  Unrolled by two so that each parity reads with its own address table; the
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             if (k + 1 == K)
                 break;
         }
-        line_finish<Alg, OUT_ALIGNED>(st, w0, w1, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
+        line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
         g = gn;
         if (g >= n_groups)
             break;

@@ -175,7 +175,9 @@ __global__ __launch_bounds__(256, 1) void digest_line1_kernel(const uint8_t *__r
                 break;
         }
     }
-    line_finish<Alg, OUT_ALIGNED>(st, w0, w1, t, nfull, K, rec_len, out, r0 + lane, n_rec);
+    uint32_t tm[16], tp[16];
+    tail_masks(t, tm, tp);
+    line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, r0 + lane, n_rec);
     BRB_LINE_PROBE(3);
 }
 
