@@ -140,6 +140,24 @@ def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
+@pytest.mark.parametrize("n,rec_len,off", [
+    (1, 4, 0), (63, 8, 4), (64, 64, 8), (65, 60, 12), (1000, 56, 0), (1001, 52, 4),
+    (4097, 12, 0), (300_001, 32, 4), (270_000, 64, 0), (5000, 16, 8), (5000, 20, 0), (5000, 44, 12),
+])
+def test_short_records_exact_buffer(brb, orc, torch_dev, n, rec_len, off):
+    """Records of at most 64 B at 4-byte bases (one compression + padding, or two when the tail
+    holds 56..63 bytes) in a device buffer that ends exactly at the batch, so the staging's range
+    check is what zeroes the bytes past the last record; n > 262 144 gives several groups per wave."""
+    data = workload.gen_records(0x5EED000C, 0, n, rec_len)
+    d = torch_dev.zeros(off + data.size, dtype=torch_dev.uint8, device="cuda")
+    d[off:] = to_dev(torch_dev, data)
+    view = d[off:]
+    assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.md5_batch_fixed(data, rec_len, n, threads=16))
+    assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+
+
 def test_cfg5_full_shard(brb, orc, torch_dev, golden):
     """cfg5 as configured: GPU 7's whole shard of the 8 388 608-record batch (records [7/8 N, N),
     1 048 576 x 1500 B = 1.57 GB, HBM-resident), every digest against the oracle, and both ends of
