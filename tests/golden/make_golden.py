@@ -211,6 +211,120 @@ def check_blowfish64(bf: dict) -> None:
     assert [hex(v) for v in ct[:16]] == g["cipher_first8"]
 
 
+# ---- second derivations of the other oracle-only fixtures (quirks.json) ----
+M32 = 0xFFFFFFFF
+
+
+class ByteArraySha1:
+    """BrbSha1_Init/Update/Final (sha1.c:132-200) on a caller-owned bytearray, written from the
+    reference text independently of the oracle: Transform (:75-130) works IN the 64 bytes it is
+    given, blk0 (:46-47) stores each byte-swapped word back and blk (:49-50) stores W[i] over
+    l[i & 15], so a block hashed straight from the caller's data (:157-158) is left holding
+    W[64..79] as little-endian words.  count[0] is 32 bits and compared with the 64-bit len << 3
+    (:152), the spurious carry for single updates of 2^29 bytes or more."""
+
+    def __init__(self):
+        self.state = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+        self.count = [0, 0]
+        self.buffer = bytearray(64)
+
+    def _transform(self, mem: bytearray, off: int) -> None:
+        l = [int.from_bytes(mem[off + 4 * k: off + 4 * k + 4], "little") for k in range(16)]
+        rol = lambda v, n: ((v << n) | (v >> (32 - n))) & M32
+        a, b, c, d, e = self.state
+        for i in range(80):
+            if i < 16:
+                l[i] = int.from_bytes(l[i].to_bytes(4, "little"), "big")       # blk0: byte swap in place
+            else:
+                l[i & 15] = rol(l[(i + 13) & 15] ^ l[(i + 8) & 15] ^ l[(i + 2) & 15] ^ l[i & 15], 1)
+            if i < 20:
+                f, k = (b & (c ^ d)) ^ d, 0x5A827999
+            elif i < 40:
+                f, k = b ^ c ^ d, 0x6ED9EBA1
+            elif i < 60:
+                f, k = ((b | c) & d) | (b & c), 0x8F1BBCDC
+            else:
+                f, k = b ^ c ^ d, 0xCA62C1D6
+            e, d, c, b, a = d, c, rol(b, 30), a, (e + f + l[i & 15] + k + rol(a, 5)) & M32
+        for k in range(16):
+            mem[off + 4 * k: off + 4 * k + 4] = l[k].to_bytes(4, "little")
+        self.state = [(x + y) & M32 for x, y in zip(self.state, (a, b, c, d, e))]
+
+    def update(self, data: bytearray, length: int) -> None:
+        j = (self.count[0] >> 3) & 63
+        bits = length << 3                                  # size_t
+        self.count[0] = (self.count[0] + bits) & M32
+        if self.count[0] < bits:
+            self.count[1] = (self.count[1] + 1) & M32
+        self.count[1] = (self.count[1] + (length >> 29)) & M32
+        if j + length > 63:
+            i = 64 - j
+            self.buffer[j:64] = data[:i]
+            self._transform(self.buffer, 0)
+            while i + 63 < length:
+                self._transform(data, i)                    # in the caller's memory
+                i += 64
+            j = 0
+        else:
+            i = 0
+        self.buffer[j:j + length - i] = data[i:length]
+
+    def final(self) -> bytes:
+        fc = bytes((self.count[0 if i >= 4 else 1] >> ((3 - (i & 3)) * 8)) & 255 for i in range(8))
+        self.update(bytearray(b"\x80"), 1)
+        while (self.count[0] & 504) != 448:
+            self.update(bytearray(1), 1)
+        self.update(bytearray(fc), 8)
+        return b"".join(v.to_bytes(4, "big") for v in self.state)
+
+
+def membuffer_key(seed: int) -> bytes:
+    """The 16 unsigned ints of mem_buf.c:1511-1515 / 1565-1569 (seed carried from word to word)."""
+    out, s = [], seed & M32
+    for i in range(16):
+        k = ((i + s) * s + 13 * i) & M32
+        out.append(k)
+        s = (k * s) & M32
+    return b"".join(k.to_bytes(4, "little") for k in out)
+
+
+def membuffer_crypt(buf: bytearray, size: int, seed: int, offset: int, decrypt: bool) -> int:
+    """MemBufferEncryptData / MemBufferDecryptData (mem_buf.c:1499-1617) on an already grown,
+    zero-filled buffer, on BigIntBlowfish: the key is used with keyLen sizeof(enc_key[16]) = 4 to
+    encrypt and sizeof(enc_key) = 64 to decrypt; blocks = size / 8 + 2 words from byte `offset`;
+    decryption stops at the first pair with a zero word.  Returns the new MemBuffer size."""
+    key = membuffer_key(seed)
+    bf = BigIntBlowfish(key, 64 if decrypt else 4)
+    blocks = (size - offset if decrypt else size + offset) // 8 + 2
+    word = lambda k: int.from_bytes(buf[offset + 8 * k: offset + 8 * k + 8], "little")
+    i = 0
+    while i < blocks:
+        xl, xr = word(i), word(i + 1)
+        if decrypt and (xl == 0 or xr == 0):
+            break
+        xl, xr = bf.decrypt(xl, xr) if decrypt else bf.encrypt(xl, xr)
+        buf[offset + 8 * i: offset + 8 * i + 16] = xl.to_bytes(8, "little") + xr.to_bytes(8, "little")
+        i += 2
+    return i * 8 + offset
+
+
+def check_quirks(q: dict) -> None:
+    """Asserts that the second derivations above reproduce every byte of a quirks.json dict."""
+    s = q["sha1_inplace"]
+    msg = bytearray.fromhex(s["input"])
+    h = ByteArraySha1()
+    h.update(msg, len(msg))
+    assert msg.hex() == s["after_update"]
+    assert h.final().hex() == s["digest"] == s["hashlib_digest"]
+    assert membuffer_key(0x4FD9).hex() == q["membuf_key_4fd9"]
+    for m in q["membuffer"]:
+        enc = bytearray.fromhex(m["plain"])
+        assert membuffer_crypt(enc, m["size"], m["seed"], m["offset"], False) == m["enc_size"]
+        assert enc.hex() == m["enc"]
+        assert membuffer_crypt(enc, m["enc_size"], m["seed"], m["offset"], True) == m["dec_size"]
+        assert enc.hex() == m["dec"]
+
+
 def dump(name, obj):
     with open(os.path.join(OUT, name), "w") as f:
         json.dump(obj, f, indent=1, sort_keys=True)
@@ -301,13 +415,17 @@ def main():
         dec_size = oracle.membuf_decrypt(dec, new_size, seed_, off)
         mb.append({"size": size, "offset": off, "seed": seed_, "plain": bytes(buf).hex(),
                    "enc_size": int(new_size), "enc": bytes(enc).hex(), "dec_size": int(dec_size), "dec": bytes(dec).hex()})
-    dump("quirks.json", {
+    quirks = {
         "source": "oracle",
         "sha1_inplace": {"input": before.hex(), "after_update": bytes(msg).hex(), "digest": dig.raw.hex(),
                          "hashlib_digest": hashlib.sha1(before).hexdigest()},
         "membuffer": mb,
         "membuf_key_4fd9": oracle.membuf_key(0x4FD9).hex(),
-    })
+    }
+    check_quirks(quirks)     # second derivation: ByteArraySha1 and membuffer_crypt reproduce every byte
+    quirks["second_derivation"] = ("tests/golden/make_golden.py ByteArraySha1 (sha1.c on a Python bytearray) and "
+                                   "membuffer_crypt (mem_buf.c:1499-1617 on BigIntBlowfish) reproduce every byte above")
+    dump("quirks.json", quirks)
     # ---- RC4 and the RC4+MD5 frame ----
     for k, p_, c in RC4_KAT:
         key, pt = bytes.fromhex(k), bytes.fromhex(p_)

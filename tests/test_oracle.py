@@ -146,6 +146,26 @@ def test_blowfish64_second_derivation(golden):
     mg.check_blowfish64(golden["blowfish64"])
 
 
+def test_quirks_second_derivation(golden):
+    """The other oracle-only fixtures, two-source as well: make_golden.py's ByteArraySha1 (sha1.c:75-200
+    rewritten on a Python bytearray, in-place block writes and the 32-bit count included) and
+    membuffer_crypt (mem_buf.c:1499-1617 on BigIntBlowfish) reproduce the SHA-1 mutation bytes,
+    the digest, the MemBuffer key and every MemBuffer encrypt/decrypt image and size."""
+    import hashlib
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(os.path.dirname(__file__), "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    mg.check_quirks(golden["quirks"])
+    for n in (0, 1, 55, 56, 63, 64, 65, 200, 1000):           # and it is SHA-1 (hashlib)
+        m = bytearray((i * 7 + 3) & 255 for i in range(n))
+        h = mg.ByteArraySha1()
+        h.update(bytearray(m), n)
+        assert h.final() == hashlib.sha1(bytes(m)).digest(), n
+
+
 def test_sha1_inplace_quirk(orc, golden):
     """BrbSha1_Update rewrites full blocks taken straight from `data` (sha1.c:84-90,157-158):
     for a 200-byte single update, bytes 64..191 change and 0..63 / 192..199 do not."""
