@@ -121,8 +121,10 @@ def compute_fraction(path, key, launch_s, cyc_lone):
     """roofline.compute: the VALU-issue ceiling.  insts = SQ_INSTS_VALU per dispatch (rocprofv3
     --pmc, chip-wide sum of wave-instructions); per SIMD = insts / 1024.  frac_peak = that many
     instructions at the SIMD's peak issue (2 cycles per wave64 instruction) and 2.4 GHz over the
-    launch time; frac_lone_wave = the same at the issue cost one wave per SIMD measured (cfg2 and
-    the one-wave-per-SIMD kernels run that way)."""
+    launch time; frac_lone_wave = the same at the cost per instruction measured for the kernel's
+    step mix at one wave per SIMD (tools/mb/valu_latency.hip).  That cost is close to the SIMD's
+    rate for the mix at any wave count: MD5 hashing alone runs 23.4 us at one wave per SIMD and
+    22.0 us at eight (tools/mb/small_probe.hip), so it is the compute ceiling of cfg3/cfg5 too."""
     _, det = load_pmc(path, key)
     if not det or "sq_insts_valu" not in det:
         return None
@@ -135,6 +137,8 @@ def compute_fraction(path, key, launch_s, cyc_lone):
     if cyc_lone:
         out["lone_wave_cycles_per_inst"] = cyc_lone
         out["frac_lone_wave"] = round(per_simd * cyc_lone / cyc, 4)
+        out["note"] = ("frac_lone_wave: VALU per SIMD x the step mix's measured cycles per instruction "
+                       "(one wave per SIMD; eight waves per SIMD hash only ~6% faster) / launch cycles at 2.4 GHz")
     return out
 
 

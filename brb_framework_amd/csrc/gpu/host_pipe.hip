@@ -349,7 +349,8 @@ int split_devices(uint64_t n, const std::function<int(int, uint64_t, uint64_t)> 
         pending.add();
         worker(g, 0).post([&, g, lo, hi] {
             brb_api::clear_err();
-            res[g].rc = part(g, lo, hi);
+            DeviceGuard dg{g};                         // the worker selected g at start; a failure there shows here
+            res[g].rc = dg.error() != hipSuccess ? fail_hip("hipSetDevice", dg.error()) : part(g, lo, hi);
             if (res[g].rc != BRB_BATCH_OK)
                 res[g].err = brb_api::t_err;
             pending.done(BRB_BATCH_OK, std::string());
