@@ -44,6 +44,8 @@ from .crypto import (  # noqa: F401
     md5_batch,
     md5_batch_fixed,
     md5_batch_segments,
+    metadata_unpack_batch,
+    METADATA_INFO_DTYPE,
     membuf_decrypt,
     membuf_encrypt,
     membuf_key,
@@ -64,7 +66,7 @@ __all__ = [
     "blowfish_init", "exported_symbols", "gpu_available", "lib", "md5_batch", "md5_batch_fixed",
     "sha1_batch", "sha1_batch_fixed", "BRB_RC4_State", "RC4_STATE_BYTES", "RC4MD5_HEADER", "rc4_crypt_batch",
     "rc4_init", "rc4_state_bytes", "rc4_states", "rc4md5_frame_batch", "rc4md5_open_batch", "membuf_decrypt",
-    "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "base64_decode_batch",
+    "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "metadata_unpack_batch", "METADATA_INFO_DTYPE", "base64_decode_batch",
     "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
     "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED", "BATCH_ALL_DEVICES", "device_count",
 ]

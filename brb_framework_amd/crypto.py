@@ -81,6 +81,9 @@ _SIGNATURES = [
     ("BRB_MD5BatchSegments", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
       ctypes.c_uint, ctypes.c_void_p]),
+    ("BRB_MetaDataUnpackBatch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint,
+      ctypes.c_void_p]),
     ("BrbSha1_BatchFixed", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]),
     ("BrbSha1_Batch", ctypes.c_int,
@@ -264,6 +267,28 @@ def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, 
     flags, h = _mode(data, stream, async_)
     _check(lib().BRB_MD5BatchSegments(_ptr(data), _ptr(seg_offsets), _ptr(seg_lengths), _ptr(rec_first_seg), n,
                                       _ptr(out), flags, h), "BRB_MD5BatchSegments")
+    return out
+
+
+# BRB_MetaDataUnpackInfo (include/brb_crypto.h), one per pack
+METADATA_INFO_DTYPE = np.dtype([("error_code", "<i4"), ("item_count", "<u4"), ("cur_offset", "<u8"),
+                                ("cur_remaining", "<u8"), ("cur_needed", "<u8")])
+
+
+def metadata_unpack_batch(data, offsets, lengths, out=None, stream=None, async_=False, all_devices=False):
+    """BRB_MetaDataUnpackBatch: MetaDataUnpack (meta_data.c:145-328) of pack i = data[offsets[i] ..
+    + lengths[i]); returns one BRB_MetaDataUnpackInfo per pack (numpy structured array in host mode,
+    an (n, 32) uint8 tensor in device mode)."""
+    n = len(offsets)
+    if out is None:
+        if _is_torch(data):
+            import torch
+            out = torch.empty((n, METADATA_INFO_DTYPE.itemsize), dtype=torch.uint8, device=data.device)
+        else:
+            out = np.empty(n, METADATA_INFO_DTYPE)
+    flags, h = _mode(data, stream, async_, all_devices)
+    _check(lib().BRB_MetaDataUnpackBatch(_ptr(data), _ptr(offsets), _ptr(lengths), n, _ptr(out), flags, h),
+           "BRB_MetaDataUnpackBatch")
     return out
 
 

@@ -587,6 +587,54 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
     return rc;
 }
 
+// ---- MetaData packs ------------------------------------------------------------
+int metadata_unpack(const void *data, const uint64_t *offs, const uint32_t *lens, uint64_t n,
+                    BRB_MetaDataUnpackInfo *info, unsigned flags, void *stream)
+{
+    t_err.clear();
+    if (n == 0)
+        return BRB_BATCH_OK;
+    if (!data || !offs || !lens || !info) {
+        set_err("NULL data, offsets, lengths or info");
+        return BRB_BATCH_BADARG;
+    }
+    if (!items_ok(n) || !flags_ok(flags))
+        return BRB_BATCH_BADARG;
+    if (int ok = device_ok(); ok != BRB_BATCH_OK)
+        return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES)   // contiguous pack ranges, one per device
+        return brb_host::split_devices(n, [&](int, uint64_t lo, uint64_t hi) {
+            return metadata_unpack(data, offs + lo, lens + lo, hi - lo, info + lo, flags & ~BRB_BATCH_ALL_DEVICES, nullptr);
+        });
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (flags & BRB_BATCH_DEVICE) {
+        if ((e = brb::launch_metadata_unpack(static_cast<const uint8_t *>(data), offs, lens, n, info, s)) != hipSuccess)
+            return fail_hip("kernel launch", e);
+        return finish(s, flags);
+    }
+    // host mode: copy the byte span the packs cover, with the offsets rebased to it
+    uint64_t lo, hi;
+    if (!span_of(offs, lens, n, 0, lo, hi))
+        return BRB_BATCH_BADARG;
+    const std::vector<uint64_t> roff = rebase(offs, n, lo);
+    Staging st;
+    const size_t i_d = st.add(static_cast<const uint8_t *>(data) + lo, nullptr, size_t(hi - lo));
+    const size_t i_o = st.add(roff.data(), nullptr, 8 * n);
+    const size_t i_l = st.add(lens, nullptr, 4 * n);
+    const size_t i_out = st.add(nullptr, info, sizeof(BRB_MetaDataUnpackInfo) * n);
+    int rc = st.upload(s);
+    if (rc == BRB_BATCH_OK &&
+        (e = brb::launch_metadata_unpack(st.dev(i_d), reinterpret_cast<const uint64_t *>(st.dev(i_o)),
+                                         reinterpret_cast<const uint32_t *>(st.dev(i_l)), n,
+                                         reinterpret_cast<BRB_MetaDataUnpackInfo *>(st.dev(i_out)), s)) != hipSuccess)
+        rc = fail_hip("kernel launch", e);
+    if (rc == BRB_BATCH_OK)
+        return st.download(s);
+    (void)hipStreamSynchronize(s);
+    return rc;
+}
+
 // ---- base64 --------------------------------------------------------------------
 int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, void *out,
               const uint64_t *ooffs, uint32_t *olens, unsigned flags, void *stream)
@@ -757,6 +805,12 @@ int BRB_MD5BatchSegments(const void *data, const uint64_t *seg_offsets, const ui
                          void *hip_stream)
 {
     return md5_segments(data, seg_offsets, seg_lengths, rec_first_seg, n_rec, digests, flags, hip_stream);
+}
+
+int BRB_MetaDataUnpackBatch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n_packs,
+                            BRB_MetaDataUnpackInfo *info, unsigned flags, void *hip_stream)
+{
+    return metadata_unpack(data, offsets, lengths, n_packs, info, flags, hip_stream);
 }
 
 int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec, uint8_t (*digests)[20], unsigned flags,

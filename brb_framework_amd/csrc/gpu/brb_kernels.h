@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "brb_crypto.h"
 #include "brb_gpu_common.h"
 
 namespace brb {
@@ -23,6 +24,10 @@ hipError_t launch_first_zero_pair(const uint64_t *words, uint64_t n_blocks, unsi
 // MD5 of segment lists (md5_seg_kernels.hip): record r = segments first[r] .. first[r + 1] - 1
 hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const uint32_t *slen, const uint64_t *first,
                                uint64_t n_rec, uint8_t *out, hipStream_t s);
+
+// MetaDataUnpack of whole packs (metadata_kernels.hip): pack r = data[offs[r] .. + lens[r])
+hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, const uint32_t *lens, uint64_t n,
+                                  BRB_MetaDataUnpackInfo *info, hipStream_t s);
 
 // base64 (base64_kernels.hip)
 hipError_t launch_b64_encode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,

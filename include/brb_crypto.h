@@ -148,6 +148,37 @@ int BRB_MD5BatchSegments(const void *data, const uint64_t *seg_offsets, const ui
                          const uint64_t *rec_first_seg, uint64_t n_rec, unsigned char (*digests)[16],
                          unsigned flags, void *hip_stream);
 
+/* MetaData packs (the format of meta_data.c:104-140, libbrb_data.h:291-330, LP64):
+ * a 64-byte header {int version; int item_count; unsigned long size; "BRB_META"; 16-byte MD5 of
+ * the items' data; 24 reserved bytes}, then per item {unsigned long item_id, item_sub_id, sz;
+ * sz data bytes; 0x1F}.  BRB_MetaDataUnpackBatch checks pack i = data[offsets[i] .. + lengths[i])
+ * exactly as MetaDataUnpack (meta_data.c:145-328) checks a MemBuffer holding it at offset 0, and
+ * writes the MetaDataUnpackerInfo fields (libbrb_data.h:332-344) plus the number of items unpacked:
+ * error_code is a BRB_METADATA_UNPACK_* value (the reference's MetaDataUnpackReturnCode), SUCCESS
+ * only if every canary holds and the MD5 of the items read equals the header's digest.  Quirks kept:
+ * an item is only read with sizeof(MetaDataItem) = 32 bytes left (24 are its header), so a pack whose
+ * last item holds 0..6 data bytes reports NEED_MORE_DATA_METAITEM; the walk stops after item_count
+ * items or at the pack's end, whichever comes first.  Where the reference reads past its buffer
+ * (packs shorter than the header, a size field beyond the pack), bytes past the pack read as 0 and
+ * an item larger than the whole pack reports NEED_MORE_DATA_OBJECT without being read. */
+#define BRB_METADATA_UNPACK_FAILED_INVALID_HEADER_MAGIC 0
+#define BRB_METADATA_UNPACK_FAILED_CORRUPTED_CANARY 3
+#define BRB_METADATA_UNPACK_FAILED_DIGEST_INVALID 4
+#define BRB_METADATA_UNPACK_FAILED_NEED_MORE_DATA_METAITEM 5
+#define BRB_METADATA_UNPACK_FAILED_NEED_MORE_DATA_OBJECT 6
+#define BRB_METADATA_UNPACK_SUCCESS 7
+#define BRB_METADATA_HEADER_SIZE 64
+#define BRB_METADATA_ITEM_RAW_SIZE 24
+typedef struct BRB_MetaDataUnpackInfo {
+    int32_t error_code;       /* MetaDataUnpackReturnCode */
+    uint32_t item_count;      /* items whose canary was checked before error_code was decided */
+    uint64_t cur_offset;      /* MetaDataUnpackerInfo.cur_offset / cur_remaining / cur_needed */
+    uint64_t cur_remaining;
+    uint64_t cur_needed;
+} BRB_MetaDataUnpackInfo;
+int BRB_MetaDataUnpackBatch(const void *data, const uint64_t *offsets, const uint32_t *lengths, uint64_t n_packs,
+                            BRB_MetaDataUnpackInfo *info, unsigned flags, void *hip_stream);
+
 /* SHA-1 batches: digests[i] = BrbSha1_Do(record i) (20 raw big-endian bytes).  Unlike
  * BrbSha1_Update the batch surface never writes into the input records. */
 int BrbSha1_BatchFixed(const void *data, uint32_t rec_len, uint64_t n_rec,

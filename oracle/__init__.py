@@ -53,6 +53,8 @@ def lib() -> ctypes.CDLL:
             "orc_rc4md5_open_batch": (None, [vp, vp, vp, vp, u64, vp, ctypes.c_int]),
             "orc_b64_encode": (u64, [vp, u64, vp]),
             "orc_b64_decode": (u64, [vp, u64, vp]),
+            "orc_metadata_pack": (u64, [vp, vp, vp, vp, vp, u64, vp]),
+            "orc_metadata_unpack": (ctypes.c_int, [vp, u64, vp]),
             "orc_splitmix64": (u64, [u64]),
             "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
         }
@@ -230,6 +232,33 @@ def b64_decode(text: bytes) -> bytes:
 
 
 # ---- generator ---------------------------------------------------------------
+class MdInfo(ctypes.Structure):
+    _fields_ = [("error_code", ctypes.c_int32), ("item_count", ctypes.c_uint32), ("cur_offset", ctypes.c_uint64),
+                ("cur_remaining", ctypes.c_uint64), ("cur_needed", ctypes.c_uint64)]
+
+
+def metadata_pack(items) -> bytes:
+    """MetaDataPack (meta_data.c:104-140): items = [(item_id, item_sub_id, data bytes), ...]."""
+    data = b"".join(d for _, _, d in items)
+    lens = np.array([len(d) for _, _, d in items], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if len(items) else np.zeros(0, np.uint64)
+    ids = np.array([i for i, _, _ in items], np.uint64)
+    subs = np.array([s for _, s, _ in items], np.uint64)
+    src = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    out = np.zeros(64 + int(lens.sum()) + 25 * len(items), np.uint8)
+    ptr = lambda a: a.ctypes.data if a.size else None
+    n = lib().orc_metadata_pack(_p(src), ptr(offs), ptr(lens), ptr(ids), ptr(subs), len(items), _p(out))
+    return out[:n].tobytes()
+
+
+def metadata_unpack(pack: bytes) -> tuple:
+    """MetaDataUnpack (meta_data.c:145-328) -> (error_code, item_count, cur_offset, cur_remaining, cur_needed)."""
+    b = np.frombuffer(pack, np.uint8) if pack else np.zeros(1, np.uint8)
+    info = MdInfo()
+    lib().orc_metadata_unpack(_p(b), len(pack), ctypes.byref(info))
+    return (info.error_code, info.item_count, info.cur_offset, info.cur_remaining, info.cur_needed)
+
+
 def gen_records(seed: int, r0: int, n: int, rec_len: int) -> np.ndarray:
     """C restatement of the deterministic byte generator: n records of rec_len bytes."""
     out = np.empty(n * rec_len, np.uint8)

@@ -678,6 +678,123 @@ uint64_t orc_b64_decode(const char *in, uint64_t len, uint8_t *out)
 }
 
 /* =========================================================================================== */
+/* MetaData packs -- libbrb_core/data/utils/meta_data.c, libbrb_data.h:291-330 (LP64)           */
+/* =========================================================================================== */
+/* header: int version @0, int item_count @4, unsigned long size @8, "BRB_META" @16, MD5 @24,
+ * 24 reserved bytes @40; item: unsigned long item_id, item_sub_id, sz; data; 0x1F */
+static void put_le(uint8_t *p, uint64_t v, int n)
+{
+    for (int k = 0; k < n; k++)
+        p[k] = (uint8_t)(v >> (8 * k));
+}
+
+/* MetaDataPack (meta_data.c:104-140) with MetaDataHeaderLoadData (:397-433): returns the bytes written */
+uint64_t orc_metadata_pack(const uint8_t *data, const uint64_t *off, const uint64_t *len, const uint64_t *id,
+                           const uint64_t *sub, uint64_t n_items, uint8_t *out)
+{
+    orc_md5_ctx c;
+    memset(&c, 0, sizeof(c));
+    orc_md5_init(&c);
+    uint64_t size = 0;
+    for (uint64_t i = 0; i < n_items; i++) {
+        orc_md5_update_big(&c, data + off[i], (unsigned long)len[i]);
+        size += len[i] + 24 + 1;
+    }
+    orc_md5_final(&c);
+    memset(out, 0, 64);
+    put_le(out + 4, (uint32_t)(int32_t)n_items, 4);
+    put_le(out + 8, size, 8);
+    memcpy(out + 16, "BRB_META", 8);
+    memcpy(out + 24, c.digest, 16);
+    uint64_t o = 64;
+    for (uint64_t i = 0; i < n_items; i++) {
+        put_le(out + o, id[i], 8);
+        put_le(out + o + 8, sub[i], 8);
+        put_le(out + o + 16, len[i], 8);
+        memcpy(out + o + 24, data + off[i], len[i]);
+        out[o + 24 + len[i]] = 0x1F;
+        o += 24 + len[i] + 1;
+    }
+    return o;
+}
+
+/* a byte of the pack, 0 past its end (the reference reads whatever its MemBuffer holds there) */
+static uint8_t md_byte(const uint8_t *b, uint64_t size, uint64_t pos) { return pos < size ? b[pos] : 0; }
+static uint64_t md_u64(const uint8_t *b, uint64_t size, uint64_t pos)
+{
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++)
+        v |= (uint64_t)md_byte(b, size, pos + (uint64_t)k) << (8 * k);
+    return v;
+}
+
+/* MetaDataUnpack (meta_data.c:145-328) of a MemBuffer holding the pack at offset 0; info = the
+ * MetaDataUnpackerInfo fields plus the count of items unpacked.  Returns error_code. */
+int orc_metadata_unpack(const uint8_t *b, uint64_t size, orc_md_info *info)
+{
+    uint64_t cur_offset = 0, cur_remaining = 0, cur_needed = 0, pos = 0;
+    uint32_t items = 0;
+    int code = 7;                                                    /* METADATA_UNPACK_SUCCESS */
+    const int32_t item_count = (int32_t)(uint32_t)(md_u64(b, size, 0) >> 32);
+    if (md_u64(b, size, 16) != md_u64((const uint8_t *)"BRB_META", 8, 0)) {   /* :183-195 */
+        code = 0;
+        goto out;
+    }
+    orc_md5_ctx c;
+    memset(&c, 0, sizeof(c));
+    orc_md5_init(&c);
+    pos = 64;                                                        /* :198-199 */
+    cur_offset += 64;
+    for (int32_t i = 0; i < item_count; i++) {                       /* :202 */
+        cur_remaining = size - pos;                                  /* :213 */
+        if (cur_remaining < 32) {                                    /* :216-224, sizeof(MetaDataItem) */
+            cur_needed = 32 - cur_remaining;
+            code = 5;
+            goto out;
+        }
+        const uint64_t sz = md_u64(b, size, pos + 16);
+        pos += 24;                                                   /* :227-232 */
+        cur_offset += 24;
+        cur_remaining -= 24;
+        if (cur_remaining < sz + 1 || sz > size) {                   /* :237-246 */
+            cur_needed = sz + 1 - cur_remaining;
+            code = 6;
+            goto out;
+        }
+        for (uint64_t k = 0; k < sz; k++) {                          /* :249-254 */
+            uint8_t v = md_byte(b, size, pos + k);
+            orc_md5_update_big(&c, &v, 1);
+        }
+        pos += sz;
+        cur_offset += sz;
+        cur_remaining -= sz;
+        if (md_byte(b, size, pos) != 0x1F) {                         /* :258-268 */
+            code = 3;
+            goto out;
+        }
+        pos += 1;                                                    /* :271-277 */
+        cur_offset += 1;
+        cur_remaining -= 1;
+        items++;
+        if (pos == size)                                             /* :280-281 */
+            break;
+    }
+    orc_md5_final(&c);                                               /* :285-298 */
+    for (int k = 0; k < 16; k++)
+        if (c.digest[k] != md_byte(b, size, 24 + (uint64_t)k)) {
+            code = 4;
+            break;
+        }
+out:
+    info->error_code = code;
+    info->item_count = items;
+    info->cur_offset = cur_offset;
+    info->cur_remaining = cur_remaining;
+    info->cur_needed = cur_needed;
+    return code;
+}
+
+/* =========================================================================================== */
 /* Generator                                                                                     */
 /* =========================================================================================== */
 uint64_t orc_splitmix64(uint64_t x)

@@ -130,6 +130,16 @@ void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *le
 uint64_t orc_splitmix64(uint64_t x);
 void orc_gen_records(uint64_t seed, uint64_t r0, uint64_t n, uint32_t rec_len, uint8_t *out);
 
+/* MetaData packs (meta_data.c:104-140, 145-328, 397-433) */
+typedef struct {
+    int32_t error_code;
+    uint32_t item_count;
+    uint64_t cur_offset, cur_remaining, cur_needed;
+} orc_md_info;
+uint64_t orc_metadata_pack(const uint8_t *data, const uint64_t *off, const uint64_t *len, const uint64_t *id,
+                           const uint64_t *sub, uint64_t n_items, uint8_t *out);
+int orc_metadata_unpack(const uint8_t *b, uint64_t size, orc_md_info *info);
+
 #ifdef __cplusplus
 }
 #endif
