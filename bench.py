@@ -52,8 +52,9 @@ def parse():
                     help="untimed warm-up steps W (default: as many as fill >= 1 s, so the GPU clock has "
                          "ramped up before the timed region)")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher"],
-                    help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B)")
+    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher", "metadata", "base64"],
+                    help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B); "
+                         "metadata / base64: f4 on the same shape")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the timed steps alternate over")
     ap.add_argument("--two-stream", action="store_true", help="also time the steps over 2 streams")
@@ -199,6 +200,8 @@ def main():
         result = bench_batcher(args, rank, world, log)
     elif args.op in ("rc4", "rc4md5"):
         result = bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
+    elif args.op in ("metadata", "base64"):
+        result = bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif cfg["op"] == "blowfish":
         result = bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
     else:
@@ -789,6 +792,139 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                                   "nproc_note": "threads = the lease's CPU share (see the digest line's cores_note)",
                                   "kind": "port",
                                   "sample": f"oracle frame+open of {m} connections x {L} B, {reps} passes, {th} pthreads"}
+    log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")
+    return result
+
+
+def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
+    """SURVEY §8 f4 on the cfg2 shape (65 536 records of 1500 data bytes per GPU, HBM-resident).
+    --op metadata: one step = BRB_MetaDataUnpackBatch over 65 536 MetaData packs of 4 items x 375 B
+                   (1 664 bytes each: header, item headers, data, canaries), every pack valid.
+    --op base64:   one step = BRB_Base64EncodeBatch of the 1500-byte records (2000 characters each),
+                   then BRB_Base64DecodeBatch of those texts back into 1500-byte records."""
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+    import oracle
+
+    L = 1500
+    n = args.records_per_gpu or 65536
+    host = workload.gen_records(workload.SEEDS[2], rank * n, n, L)
+    Lb = brb.lib()
+    flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
+    if args.op == "metadata":
+        K, Q = 4, L // 4                         # items per pack, bytes per item
+        P_SZ = 64 + K * (24 + Q + 1)
+        packs = np.zeros((n, P_SZ), np.uint8)
+        hdr = np.zeros(64, np.uint8)
+        hdr[:24] = np.frombuffer(np.array([0, K], "<i4").tobytes() + np.array([P_SZ - 64], "<u8").tobytes()
+                                 + b"BRB_META", np.uint8)
+        packs[:, :64] = hdr
+        packs[:, 24:40] = brb.md5_batch_fixed(host, L, n)        # MD5 of the items' concatenation
+        for j in range(K):
+            o = 64 + j * (24 + Q + 1)
+            packs[:, o:o + 24] = np.frombuffer(np.array([j + 1, 0, Q], "<u8").tobytes(), np.uint8)
+            packs[:, o + 24:o + 24 + Q] = host.reshape(n, L)[:, j * Q:(j + 1) * Q]
+            packs[:, o + 24 + Q] = 0x1F
+        flat = packs.reshape(-1)
+        offs_h = np.arange(n, dtype=np.uint64) * P_SZ
+        lens_h = np.full(n, P_SZ, np.uint32)
+        n_rot = max(2, math.ceil(640e6 / flat.nbytes))
+        bufs = [torch.from_numpy(flat).to(dev)]
+        for _ in range(n_rot - 1):
+            bufs.append(bufs[0].clone())
+        offs = torch.from_numpy(offs_h.view(np.int64)).to(dev)
+        lens = torch.from_numpy(lens_h.view(np.int32)).to(dev)
+        info = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+        bptr = [b.data_ptr() for b in bufs]
+        po, pl, pi = offs.data_ptr(), lens.data_ptr(), info.data_ptr()
+
+        def launch(k, s, j=0):
+            if Lb.BRB_MetaDataUnpackBatch(bptr[k % n_rot], po, pl, n, pi, flags, s.cuda_stream) != 1:
+                raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+        moved, payload, name = n * (P_SZ + 32), n * P_SZ, "BRB_MetaDataUnpackBatch"
+        metric = "GiB/s of MetaData packs validated (MetaDataUnpack: walk, canaries, MD5) (SURVEY §8 f4)"
+    else:
+        T = 4 * ((L + 2) // 3)
+        n_rot = max(2, math.ceil(640e6 / host.nbytes))
+        bufs = [torch.from_numpy(host).to(dev)]
+        for _ in range(n_rot - 1):
+            bufs.append(bufs[0].clone())
+        offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * L).view(np.int64)).to(dev)
+        lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        toffs = torch.from_numpy((np.arange(n, dtype=np.uint64) * T).view(np.int64)).to(dev)
+        tlens = torch.full((n,), T, dtype=torch.int32, device=dev)
+        text = torch.zeros(n * T, dtype=torch.uint8, device=dev)
+        back = torch.zeros(n * L, dtype=torch.uint8, device=dev)
+        olens = torch.zeros(n, dtype=torch.int32, device=dev)
+        bptr = [b.data_ptr() for b in bufs]
+        P = [x.data_ptr() for x in (offs, lens, toffs, tlens, text, back, olens)]
+
+        def launch(k, s, j=0):
+            h = s.cuda_stream
+            rc = Lb.BRB_Base64EncodeBatch(bptr[k % n_rot], P[0], P[1], n, P[4], P[2], flags, h)
+            if rc == 1:
+                rc = Lb.BRB_Base64DecodeBatch(P[4], P[2], P[3], n, P[5], P[0], P[6], flags, h)
+            if rc != 1:
+                raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+        moved, payload, name = n * (2 * L + 2 * T + 4), n * L, "BRB_Base64EncodeBatch + BRB_Base64DecodeBatch"
+        metric = "GiB/s of records per base64 encode + decode round trip (SURVEY §8 f4)"
+
+    n_warm, n_steps = warm_up(args, launch, [stream], torch, max_over_ranks)
+    wall, ev_s = timed_steps(lambda k, s, j: launch(k + n_warm, s, j), n_steps, [stream], barrier,
+                             max_over_ranks, torch)
+    torch.cuda.synchronize()
+    if args.op == "metadata":
+        got = info.cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+        assert (got["error_code"] == 7).all() and (got["item_count"] == 4).all(), "a pack failed to unpack"
+        assert (got["cur_offset"] == P_SZ).all()
+    else:
+        assert (olens.cpu().numpy() == L).all()
+        last = (n_warm + n_steps - 1) % n_rot
+        assert torch.equal(back, bufs[last]), "base64 round trip changed the records"
+    step_s = ev_s / n_steps
+    result = {
+        "metric": metric,
+        "value": round(payload * world * n_steps / wall / 2**30, 2),
+        "unit": "GiB/s", "n_gpus": world, "steps": n_steps, "warmup": n_warm,
+        "ms_per_step": round(wall / n_steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic (splitmix64 records, HBM-resident, {n_rot} rotating copies)",
+        "config": {"workload": f"f4 {args.op}: {n} records x {L} data bytes" + (", 1 GPU" if world == 1 else "/GPU"),
+                   "op": name + " (device mode)", "records_per_gpu": n, "record_bytes": L,
+                   "parallelism": f"record-shard x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(moved / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                     **traffic_fields(args.pmc_summary, f"f4_{args.op}"),
+                     "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
+                     "note": "algorithmic bytes read + written per step; one lane per record, so the bound "
+                             "in practice is per-lane issue (MD5 for metadata), DESIGN.md"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        th = cpu_threads()
+        m = min(n, 16384)
+        reps, t0 = 0, time.perf_counter()
+        if args.op == "metadata":
+            fl = flat[: m * P_SZ]
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                inf = oracle.metadata_unpack_batch(fl, offs_h[:m], lens_h[:m], threads=th)
+                reps += 1
+            assert (inf.view("<i4")[:, 0] == 7).all()
+            cores, sample = th, f"oracle MetaDataUnpack of {m} packs x {P_SZ} B, {reps} passes, {th} pthreads"
+        else:
+            m = min(n, 2048)
+            recs = [host[i * L:(i + 1) * L].tobytes() for i in range(m)]
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                for r in recs:
+                    assert oracle.b64_decode(oracle.b64_encode(r)) == r
+                reps += 1
+            cores, sample = 1, f"oracle encode + decode of {m} records x {L} B, {reps} passes, 1 thread"
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": round(m * L * reps / dt / 2**30, 3) if args.op == "base64"
+                                  else round(m * P_SZ * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": cores,
+                                  "kind": "port", "sample": sample}
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")
     return result
 

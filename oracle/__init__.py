@@ -55,6 +55,7 @@ def lib() -> ctypes.CDLL:
             "orc_b64_decode": (u64, [vp, u64, vp]),
             "orc_metadata_pack": (u64, [vp, vp, vp, vp, vp, u64, vp]),
             "orc_metadata_unpack": (ctypes.c_int, [vp, u64, vp]),
+            "orc_metadata_unpack_batch": (None, [vp, vp, vp, u64, vp, ctypes.c_int]),
             "orc_splitmix64": (u64, [u64]),
             "orc_gen_records": (None, [u64, u64, u64, ctypes.c_uint32, vp]),
         }
@@ -257,6 +258,13 @@ def metadata_unpack(pack: bytes) -> tuple:
     info = MdInfo()
     lib().orc_metadata_unpack(_p(b), len(pack), ctypes.byref(info))
     return (info.error_code, info.item_count, info.cur_offset, info.cur_remaining, info.cur_needed)
+
+
+def metadata_unpack_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1) -> np.ndarray:
+    """orc_metadata_unpack over many packs; rows as BRB_MetaDataUnpackInfo (32 bytes each)."""
+    info = np.zeros((len(offsets), 32), np.uint8)
+    lib().orc_metadata_unpack_batch(_p(data), _p(offsets), _p(lengths), len(offsets), _p(info), threads)
+    return info
 
 
 def gen_records(seed: int, r0: int, n: int, rec_len: int) -> np.ndarray:

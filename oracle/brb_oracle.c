@@ -761,9 +761,13 @@ int orc_metadata_unpack(const uint8_t *b, uint64_t size, orc_md_info *info)
             code = 6;
             goto out;
         }
-        for (uint64_t k = 0; k < sz; k++) {                          /* :249-254 */
-            uint8_t v = md_byte(b, size, pos + k);
-            orc_md5_update_big(&c, &v, 1);
+        if (pos + sz <= size) {                                      /* :249-254 */
+            orc_md5_update_big(&c, b + pos, (unsigned long)sz);
+        } else {                                                     /* past the pack: zeros */
+            for (uint64_t k = 0; k < sz; k++) {
+                uint8_t v = md_byte(b, size, pos + k);
+                orc_md5_update_big(&c, &v, 1);
+            }
         }
         pos += sz;
         cur_offset += sz;
@@ -792,6 +796,40 @@ out:
     info->cur_remaining = cur_remaining;
     info->cur_needed = cur_needed;
     return code;
+}
+
+typedef struct {
+    const uint8_t *data;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t p0, p1;
+    orc_md_info *info;
+} md_job;
+
+static void *md_worker(void *arg)
+{
+    md_job *j = (md_job *)arg;
+    for (uint64_t p = j->p0; p < j->p1; p++)
+        orc_metadata_unpack(j->data + j->off[p], j->len[p], &j->info[p]);
+    return NULL;
+}
+
+/* orc_metadata_unpack of n packs on n_threads pthreads (the CPU baseline of bench.py --op metadata) */
+void orc_metadata_unpack_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n,
+                               orc_md_info *info, int n_threads)
+{
+    pthread_once(&md5_once, md5_tables);
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    md_job jobs[256];
+    for (int t = 0; t < n_threads; t++) {
+        jobs[t] = (md_job){data, off, len, n * (uint64_t)t / (uint64_t)n_threads,
+                           n * (uint64_t)(t + 1) / (uint64_t)n_threads, info};
+    }
+    if (n_threads == 1) { md_worker(&jobs[0]); return; }
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, md_worker, &jobs[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
 }
 
 /* =========================================================================================== */

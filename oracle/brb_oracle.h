@@ -139,6 +139,8 @@ typedef struct {
 uint64_t orc_metadata_pack(const uint8_t *data, const uint64_t *off, const uint64_t *len, const uint64_t *id,
                            const uint64_t *sub, uint64_t n_items, uint8_t *out);
 int orc_metadata_unpack(const uint8_t *b, uint64_t size, orc_md_info *info);
+void orc_metadata_unpack_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n,
+                               orc_md_info *info, int n_threads);
 
 #ifdef __cplusplus
 }
