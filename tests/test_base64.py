@@ -97,3 +97,42 @@ def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len):
         assert int(got_len[i]) == len(w) and int(dl[i]) == len(w), i
         assert hout[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w
         assert dd[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w
+
+
+@pytest.mark.gpu
+def test_decode_falls_back_mid_record(brb, orc):
+    """Long records whose first skipped byte, NUL or '=' run comes after several 256-character
+    fast-path steps: the fast steps' output and the serial remainder must join exactly (base64.c:131-179)."""
+    rng = np.random.default_rng(9)
+    n = 400
+    texts = []
+    for i in range(n):
+        plain = rng.integers(0, 256, int(rng.integers(300, 3000)), dtype=np.uint8).tobytes()
+        t = bytearray(orc.b64_encode(plain))
+        kind = i % 5
+        at = int(rng.integers(0, len(t)))
+        if kind == 1:
+            t[at] = ord("\n")                                   # skipped: the groups after it shift by one
+        elif kind == 2:
+            t[at] = 0                                           # ends the C string
+        elif kind == 3:
+            t[at:at] = b"*#\r"                                  # three skipped bytes
+        elif kind == 4:
+            t[at] = ord("=")                                    # counts as the value 0
+        texts.append(bytes(t))
+    lens = np.array([len(t) for t in texts], np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64) + 3)[:-1]          # 3-byte gaps: every alignment
+    buf = np.zeros(int(offs[-1]) + int(lens[-1]) + 8, np.uint8)
+    for o, t in zip(offs, texts):
+        buf[int(o):int(o) + len(t)] = np.frombuffer(t, np.uint8)
+    cap = 3 * (lens // 4)
+    doffs = np.zeros(n, np.uint64)
+    doffs[1:] = np.cumsum(cap.astype(np.uint64) + 1)[:-1]
+    out = np.full(int(cap.sum()) + n + 8, 0xEE, np.uint8)
+    got = brb.base64_decode_batch(buf, offs, lens, out, doffs)
+    for i, t in enumerate(texts):
+        w = orc.b64_decode(t)
+        assert int(got[i]) == len(w), i
+        assert out[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w, i
+        assert out[int(doffs[i]) + len(w)] == 0xEE, i             # nothing written past the decoded bytes
