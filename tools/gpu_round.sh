@@ -20,7 +20,9 @@ bash tools/gpu_pmc.sh "${1:-round}/pmc2s" --config 2 --op sha1 > /dev/null && ec
 bash tools/gpu_pmc.sh "${1:-round}/pmc3" --config 3 > /dev/null && echo "pmc3 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc4" --config 4 > /dev/null && echo "pmc4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4" --op rc4 > /dev/null && echo "pmc rc4 ok" &&
-bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4md5" --op rc4md5 > /dev/null && echo "pmc rc4md5 ok"
+bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4md5" --op rc4md5 > /dev/null && echo "pmc rc4md5 ok" &&
+bash tools/gpu_pmc.sh "${1:-round}/pmc_md" --op metadata > /dev/null && echo "pmc metadata ok" &&
+bash tools/gpu_pmc.sh "${1:-round}/pmc_b64" --op base64 > /dev/null && echo "pmc base64 ok"
 rc=$?
 tail -3 "$OUT/pytest_gpu.log"
 exit $rc
