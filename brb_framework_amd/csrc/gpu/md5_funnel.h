@@ -2,28 +2,40 @@
 // message position (BRB_MD5Init, BRB_MD5UpdateBig per piece, BRB_MD5Final: md5.c:38-168).
 //
 // A 64-bit carry holds the 0..3 message bytes left over from the previous piece; whole 32-bit
-// message words go to the lane's private 64-byte block buffer in LDS, word k of lane l at
-// (k * 64 + l) * 4 -- every access of lane l hits bank l -- and a full block is compressed from
-// there.  Used by md5_seg_kernel (a record's segments) and metadata_unpack_kernel (the items of a
-// MetaData pack).
+// message words go to the lane's private 32-word ring in LDS, word k of lane l at (k * 64 + l) * 4
+// -- every access of lane l hits bank l.  put()/put4() only write words; pump() compresses the
+// oldest 16 once they are there, and must run at least once per 16 words written.  Keeping the
+// compression out of put() leaves one compress site per caller loop: with it inside, a loop of 16
+// unrolled puts inlined 16 copies of the compression (52 KB of code for metadata_unpack_kernel).
+// Used by md5_seg_kernel (a record's segments) and metadata_unpack_kernel (a pack's items).
 #pragma once
 
 #include "md5_device.h"
 
 namespace brb_md5 {
 
+constexpr uint32_t kRingWords = 32;
+
 struct Funnel {
-    uint32_t *bb;       // word k of this lane's block at bb[64 k] (LDS)
+    uint32_t *bb;       // ring word k of this lane at bb[64 k] (LDS)
     Md5State st;
     uint64_t acc, total;
-    uint32_t nacc, wpos;
+    uint32_t nacc;      // bytes held in acc (0..3)
+    uint32_t wpos;      // words written
+    uint32_t cpos;      // words compressed (a multiple of 16)
 
     BRB_DEV void init(uint32_t *lane_words)
     {
         bb = lane_words;
         st = md5_iv();
         acc = total = 0;
-        nacc = wpos = 0;
+        nacc = wpos = cpos = 0;
+    }
+
+    BRB_DEV void word(uint32_t w)
+    {
+        bb[64 * (wpos & (kRingWords - 1))] = w;
+        ++wpos;
     }
 
     // appends the low `nb` (1..4) bytes of v, least significant first
@@ -33,30 +45,50 @@ struct Funnel {
         acc |= uint64_t(v) << (8 * nacc);
         nacc += nb;
         if (nacc >= 4) {
-            bb[64 * wpos] = uint32_t(acc);
+            word(uint32_t(acc));
             acc >>= 32;
             nacc -= 4;
-            if (++wpos == 16) {
-                uint32_t w[16];
+        }
+    }
+
+    // appends 4 bytes (always completes a word)
+    BRB_DEV void put4(uint32_t v)
+    {
+        total += 4;
+        const uint64_t x = acc | (uint64_t(v) << (8 * nacc));
+        word(uint32_t(x));
+        acc = x >> 32;
+    }
+
+    BRB_DEV void load16(uint32_t (&w)[16]) const
+    {
 #pragma unroll
-                for (int i = 0; i < 16; i++)
-                    w[i] = bb[64 * i];
-                md5_compress(st, w);
-                wpos = 0;
-            }
+        for (uint32_t i = 0; i < 16; i++)
+            w[i] = bb[64 * ((cpos + i) & (kRingWords - 1))];
+    }
+
+    BRB_DEV void pump()
+    {
+        if (wpos - cpos >= 16) {
+            uint32_t w[16];
+            load16(w);
+            md5_compress(st, w);
+            cpos += 16;
         }
     }
 
     // BRB_MD5Final (md5.c:134-168): 0x80, zeros, the 64-bit bit count
     BRB_DEV Md5State finish()
     {
+        pump();
+        const uint32_t r = wpos - cpos;                   // whole words not yet compressed (0..15)
         uint32_t w[16];
-        bb[64 * wpos] = uint32_t(acc | (uint64_t(0x80) << (8 * nacc)));
-        ++wpos;
+        load16(w);
+        const uint32_t tail = uint32_t(acc | (uint64_t(0x80) << (8 * nacc)));
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++)
-            w[i] = i < wpos ? bb[64 * i] : 0u;
-        if (wpos > 14) {
+            w[i] = i < r ? w[i] : i == r ? tail : 0u;
+        if (r + 1 > 14) {
             md5_compress(st, w);
 #pragma unroll
             for (int i = 0; i < 16; i++)

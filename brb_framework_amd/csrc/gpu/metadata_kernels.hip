@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
                                                                  const uint32_t *__restrict__ lens, uint64_t n,
                                                                  BRB_MetaDataUnpackInfo *__restrict__ info)
 {
-    __shared__ uint32_t blk[kBlock / 64][16][64];
+    __shared__ uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (r >= n)
@@ -114,10 +114,17 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
                 uint32_t w[16];
                 bs.fetch(w);
                 const uint64_t left = sz - c;
+                if (left >= 64) {
 #pragma unroll
-                for (uint32_t k = 0; k < 16; k++)
-                    if (4 * uint64_t(k) < left)
-                        f.put(w[k], left - 4 * k >= 4 ? 4u : uint32_t(left - 4 * k));
+                    for (int k = 0; k < 16; k++)
+                        f.put4(w[k]);
+                } else {
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; k++)
+                        if (4 * k < left)
+                            f.put(w[k], left - 4 * k >= 4 ? 4u : uint32_t(left - 4 * k));
+                }
+                f.pump();
             }
             offset += sz;
             remaining -= sz;
