@@ -52,7 +52,8 @@ def parse():
                     help="untimed warm-up steps W (default: as many as fill >= 1 s, so the GPU clock has "
                          "ramped up before the timed region)")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "rc4", "rc4md5", "batcher", "metadata", "base64"],
+    ap.add_argument("--op", default="md5", choices=["md5", "sha1", "md5var", "sha1var", "rc4", "rc4md5", "batcher",
+                                                  "metadata", "base64"],
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B); "
                          "metadata / base64: f4 on the same shape")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
@@ -200,6 +201,8 @@ def main():
         result = bench_batcher(args, rank, world, log)
     elif args.op in ("rc4", "rc4md5"):
         result = bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
+    elif args.op in ("md5var", "sha1var"):
+        result = bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif args.op in ("metadata", "base64"):
         result = bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif cfg["op"] == "blowfish":
@@ -793,6 +796,72 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                                   "kind": "port",
                                   "sample": f"oracle frame+open of {m} connections x {L} B, {reps} passes, {th} pthreads"}
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")
+    return result
+
+
+def bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log):
+    """BRB_MD5Batch / BrbSha1_Batch (byte offsets + lengths): 65 536 records per GPU with lengths
+    uniform in [1000, 2000] bytes (1500 on average, the cfg2 volume) at arbitrary byte offsets
+    (0..15-byte gaps), as a receive round hands over buffers of different sizes."""
+    import numpy as np
+    import torch
+
+    import brb_framework_amd as brb
+    from brb_framework_amd import workload
+
+    n = args.records_per_gpu or 65536
+    rng = np.random.default_rng(0x5EED0010 + rank)
+    lens_h = rng.integers(1000, 2001, n).astype(np.uint32)
+    gaps = rng.integers(0, 16, n).astype(np.uint64)
+    offs_h = np.cumsum(gaps + np.concatenate([[0], lens_h[:-1]]).astype(np.uint64)).astype(np.uint64)
+    total = int(offs_h[-1] + lens_h[-1])
+    host = workload.gen_records(workload.SEEDS[2], rank, 1, total + 16)
+    n_rot = max(2, math.ceil(640e6 / host.nbytes))
+    bufs = [torch.from_numpy(host).to(dev)]
+    for _ in range(n_rot - 1):
+        bufs.append(bufs[0].clone())
+    width = 16 if args.op == "md5var" else 20
+    offs = torch.from_numpy(offs_h.view(np.int64)).to(dev)
+    lens = torch.from_numpy(lens_h.view(np.int32)).to(dev)
+    out = torch.empty((n, width), dtype=torch.uint8, device=dev)
+    Lb = brb.lib()
+    cfn = Lb.BRB_MD5Batch if args.op == "md5var" else Lb.BrbSha1_Batch
+    flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
+    bptr = [b.data_ptr() for b in bufs]
+    po, pl, pout = offs.data_ptr(), lens.data_ptr(), out.data_ptr()
+
+    def launch(k, s, j=0):
+        if cfn(bptr[k % n_rot], po, pl, n, pout, flags, s.cuda_stream) != 1:
+            raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+
+    n_warm, n_steps = warm_up(args, launch, [stream], torch, max_over_ranks)
+    wall, ev_s = timed_steps(lambda k, s, j: launch(k + n_warm, s, j), n_steps, [stream], barrier,
+                             max_over_ranks, torch)
+    got = out.cpu().numpy()
+    h = hashlib.md5 if args.op == "md5var" else hashlib.sha1
+    for i in list(rng.integers(0, n, 32)) + [0, n - 1]:
+        o, L = int(offs_h[i]), int(lens_h[i])
+        assert got[i].tobytes() == h(host[o:o + L].tobytes()).digest(), f"digest mismatch at {i}"
+    step_s = ev_s / n_steps
+    payload = int(lens_h.sum())
+    name = "BRB_MD5Batch" if args.op == "md5var" else "BrbSha1_Batch"
+    result = {
+        "metric": f"GiB/s of {'MD5' if args.op == 'md5var' else 'SHA-1'} over variable-length records "
+                  "(offsets + lengths, 1000-2000 B)",
+        "value": round(payload * world * n_steps / wall / 2**30, 2),
+        "unit": "GiB/s", "n_gpus": world, "steps": n_steps, "warmup": n_warm,
+        "ms_per_step": round(wall / n_steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32",
+        "data": f"synthetic (splitmix64 bytes, HBM-resident, {n_rot} rotating copies; lengths U[1000, 2000])",
+        "config": {"workload": f"{n} records x 1000-2000 B at any byte offset" + (", 1 GPU" if world == 1 else "/GPU"),
+                   "op": name + " (device mode)", "records_per_gpu": n, "record_bytes_mean": payload / n,
+                   "parallelism": f"record-shard x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(payload / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(payload / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                     **traffic_fields(args.pmc_summary, f"var_{args.op}"),
+                     "launch_us_avg": round(step_s * 1e6, 2), "bytes_per_launch": payload},
+    }
+    log(f"[bench] {name}: {step_s * 1e6:.1f} us per launch")
     return result
 
 

@@ -1,0 +1,316 @@
+// digest_var_line.h -- lane-per-record digest (MD5, SHA-1) of records given by byte offsets and
+// lengths (BRB_MD5Batch / BrbSha1_Batch), with the line-aligned LDS-DMA staging of digest_line.h.
+//
+// What differs from the fixed-stride kernel:
+//  * Each group of 64 records gets its own buffer descriptor, 4 KiB below the lowest 128-byte line
+//    its records touch; a DMA lane learns its row's line and line count from that row's lane
+//    (ds_bpermute).  A group whose lines span 2 GiB or more (32-bit voffsets) is digested by the
+//    per-lane block reader instead (digest_lane).
+//  * Records start at any byte: the window is read one dword wider and funnel-shifted by the
+//    record's byte offset (one v_alignbit_b32 per word; a 4-byte aligned record shifts by 0).
+//  * Records have their own lengths: the group runs to its longest record; a row whose record has
+//    no line left gets an out-of-range voffset (the DMA returns zeros without touching memory), a
+//    lane compresses only its own blocks, and the tail block (if any) is stashed in registers when
+//    it passes through the window and finished for all lanes at the end of the group.
+// Record r's digest = BRB_MD5Init/Update/Final (md5.c:38-168) or BrbSha1_Do (sha1.c:203-216) of
+// data[offs[r] .. offs[r] + lens[r]).
+#pragma once
+
+#include "byte_stream.h"
+#include "digest_line.h"
+
+namespace brb_digest {
+
+// The per-lane path (and the fallback of the line kernel): 64-byte blocks, the next one in flight.
+template <class Alg>
+BRB_DEV typename Alg::State digest_lane(const uint8_t *a, uint64_t len)
+{
+    typename Alg::State st = Alg::iv();
+    brb_io::BlockSrc src;
+    src.init(a, len);
+    uint32_t w[16];
+    for (uint64_t b = 0; b < (len >> 6); ++b) {
+        src.fetch(w);
+        Alg::compress(st, w);
+    }
+    src.fetch(w);                   // tail (bytes past the record read as 0)
+    brb_io::add_marker(w, len);
+    Alg::finish(st, w, uint32_t(len & 63), len);
+    return st;
+}
+
+BRB_DEV uint64_t uniform64(uint64_t v)
+{
+    return (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))))) << 32) |
+           uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))));
+}
+
+BRB_DEV uint64_t wave_min64(uint64_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+BRB_DEV uint64_t wave_max64(uint64_t v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+template <class Alg, int WAVES, bool OUT_ALIGNED>
+__global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const uint8_t *__restrict__ data,
+                                                                        const uint64_t *__restrict__ offs,
+                                                                        const uint32_t *__restrict__ lens,
+                                                                        uint64_t n_rec, uint8_t *__restrict__ out)
+{
+    constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
+    constexpr uint32_t OOB = 0x80000000u;                      // a voffset past every descriptor's range
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
+    __shared__ uint32_t next_ticket;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    if (threadIdx.x == 0)
+        next_ticket = WAVES;                                   // tickets 0 .. WAVES-1: one per wave
+    __syncthreads();
+    auto take = [&]() -> uint64_t {
+        uint32_t tk = 0;
+        if (lane == 0)
+            tk = __hip_atomic_fetch_add(&next_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tk = __builtin_amdgcn_readfirstlane(tk);
+        return uint64_t(blockIdx.x) + uint64_t(tk) * gridDim.x;
+    };
+    uint64_t g = uint64_t(blockIdx.x) + uint64_t(wv) * gridDim.x;
+    if (g >= n_groups)
+        return;
+    const uint32_t my_off = wv * 2 * SLOT;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + my_off;
+    const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    auto swz = [](uint32_t row) { return (row >> 1) & 7; };
+
+    // ---- one group's layout (Grp): this lane's record, and the group's descriptor and DMA lanes
+    struct Grp {
+        uint64_t a;          // address of this lane's record
+        uint32_t len;
+        uint32_t K;          // 2-block iterations of the group (its longest record)
+        bool line;           // false: the group's lines span >= 2 GiB, use digest_lane
+        brb_dma::v4i rs;     // descriptor of the next line to issue
+        uint32_t vq[8];      // DMA voffsets of rows 8q + lane / 8 (line 0 relative to the descriptor)
+        uint32_t lq[8];      // lines of those rows' records
+    };
+    auto setup = [&](uint64_t g, Grp &G) {
+        const uint64_t r0 = g * 64;
+        const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
+        const uint64_t r = r0 + (lane < last ? lane : last);
+        G.a = dbase + offs[r];
+        G.len = lens[r];
+        const uint64_t line = G.a & ~uint64_t(127);
+        const uint32_t lines = G.len ? uint32_t(((G.a & 127) + G.len + 127) >> 7) : 0u;
+        const uint32_t nblk = (G.len >> 6) + ((G.len & 63) ? 1u : 0u);
+        // empty records touch no line (their offsets may point anywhere): they do not widen the span
+        // (every lane holds the reduced values; readfirstlane tells the compiler they are uniform, so
+        // the descriptor and the branches on them stay scalar)
+        const uint64_t lo = uniform64(wave_min64(G.len ? line : ~uint64_t(0)));
+        const uint64_t hi = uniform64(wave_max64(G.len ? line + 128 * uint64_t(lines) : 0));
+        G.K = __builtin_amdgcn_readfirstlane(uint32_t(wave_max64((nblk + 1) >> 1)));
+        G.line = hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16);   // all empty: lane path
+        const uint64_t base = lo - 4096;
+        const uint64_t left = hi - base;
+        G.rs.x = __builtin_amdgcn_readfirstlane(int(uint32_t(base)));
+        G.rs.y = __builtin_amdgcn_readfirstlane(int(uint32_t(base >> 32) & 0xFFFF));
+        G.rs.z = __builtin_amdgcn_readfirstlane(int(left > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(left)));
+        G.rs.w = 0x00020000;
+        const uint32_t rel = uint32_t(line - lo);              // < 2^31 when G.line
+        const uint32_t l3 = lane >> 3;
+        const uint32_t g0 = 16u * ((lane & 7) ^ (l3 >> 1));   // swz(8q + l3) = (l3 >> 1) ^ 4 (q & 1)
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int src = int(8 * q + l3) * 4;               // ds_bpermute byte address of row 8q + l3
+            const uint32_t rrel = uint32_t(__builtin_amdgcn_ds_bpermute(src, int(rel)));
+            G.lq[q] = uint32_t(__builtin_amdgcn_ds_bpermute(src, int(lines)));
+            G.vq[q] = (rrel | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
+        }
+    };
+    auto issue = [&](Grp &G, uint32_t m, uint32_t slot) {     // line m of every row -> slot
+        const uint32_t lm = lds0 + slot * SLOT;
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            v[q] = m < G.lq[q] ? G.vq[q] : OOB;
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\t"
+                     "s_mov_b32 m0, %10\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %9, 0 offen nt lds\n\t"
+                     "buffer_load_dwordx4 %2, %9, 0 offen offset:1024 nt lds\n\t"
+                     "buffer_load_dwordx4 %3, %9, 0 offen offset:2048 nt lds\n\t"
+                     "buffer_load_dwordx4 %4, %9, 0 offen offset:3072 nt lds\n\t"
+                     "s_mov_b32 m0, %11\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %5, %9, 0 offen nt lds\n\t"
+                     "buffer_load_dwordx4 %6, %9, 0 offen offset:1024 nt lds\n\t"
+                     "buffer_load_dwordx4 %7, %9, 0 offen offset:2048 nt lds\n\t"
+                     "buffer_load_dwordx4 %8, %9, 0 offen offset:3072 nt lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+                       "s"(G.rs), "s"(lm), "s"(lm + 4096u)
+                     : "memory");
+        const uint64_t b = ((uint64_t(uint32_t(G.rs.y)) << 32) | uint32_t(G.rs.x)) + 128u;
+        G.rs.x = int(uint32_t(b));
+        G.rs.y = int(uint32_t(b >> 32));
+        int z = G.rs.z;
+        asm("s_sub_i32 %0, %0, 0x80\n\ts_max_i32 %0, %0, 0" : "+s"(z) : : "scc");
+        G.rs.z = z;
+    };
+    auto start = [&](Grp &G) {                                 // lines 0 and 1 of a line group
+        if (G.line) {
+            issue(G, 0, 0);
+            issue(G, 1, 1);
+        }
+    };
+
+    // window dword i (0..32) of this lane for lines (k-1, k) in slots (0, 1) [ae] and (1, 0) [ao]
+    uint32_t ae[33], ao[33];
+    auto win_setup = [&](const Grp &G) {
+        const uint32_t sh4 = uint32_t(G.a) & 124u;
+        const uint32_t fr = (my_off + lane * 128) | (swz(lane) << 4);
+#pragma unroll
+        for (uint32_t i = 0; i < 33; i++) {
+            const uint32_t q4 = sh4 + 4 * i;                   // < 256
+            ae[i] = ((q4 & 124u) ^ fr) | ((q4 & 128u) << 6);
+            ao[i] = ae[i] ^ SLOT;
+            asm volatile("" : "+v"(ao[i]));
+        }
+    };
+    uint32_t w0[16], w1[16];
+    auto read_window = [&](const uint32_t (&ad)[33], uint32_t fb) {
+        uint32_t d[33];
+#pragma unroll
+        for (int i = 0; i < 33; i++)
+            d[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            w0[i] = __builtin_amdgcn_alignbit(d[i + 1], d[i], fb);
+            w1[i] = __builtin_amdgcn_alignbit(d[i + 17], d[i + 16], fb);
+        }
+    };
+
+    Grp G, Gn;
+    setup(g, G);
+    start(G);
+    __builtin_amdgcn_sched_barrier(0);
+    for (;;) {
+        const uint64_t gn = take();
+        const uint64_t r = g * 64 + lane;
+        typename Alg::State st;
+        if (!G.line) {
+            st = digest_lane<Alg>(reinterpret_cast<const uint8_t *>(G.a), G.len);
+            if (gn < n_groups) {
+                setup(gn, Gn);
+                start(Gn);
+            }
+        } else {
+            win_setup(G);
+            const uint32_t fb = (uint32_t(G.a) & 3u) * 8u;
+            const uint32_t nfull = G.len >> 6, t = G.len & 63;
+            const uint32_t tb = t ? nfull : 0xFFFFFFFFu;       // the block holding the tail bytes
+            uint32_t wt[16];                                   // that block, stashed as it passes
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                wt[i] = 0;
+            st = Alg::iv();
+            const uint32_t K = G.K;
+            auto step = [&](uint32_t k, const uint32_t (&ad)[33], uint32_t refill_slot) {
+                brb_dma::wait_vmcnt<0>();
+                read_window(ad, fb);
+                if (k < K) {
+                    issue(G, k + 1, refill_slot);
+                } else if (gn < n_groups) {
+                    setup(gn, Gn);
+                    start(Gn);
+                }
+                const uint32_t b = 2 * k - 2;
+                if (b < nfull)
+                    Alg::compress(st, w0);
+                if (b + 1 < nfull)
+                    Alg::compress(st, w1);
+                if (__builtin_amdgcn_ballot_w64(tb - b < 2) != 0) {   // some lane's tail is in the window
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        wt[i] = tb == b ? w0[i] : tb == b + 1 ? w1[i] : wt[i];
+                }
+            };
+            if (K == 0) {                                      // every record of the group is empty
+                brb_dma::wait_vmcnt<0>();
+                if (gn < n_groups) {
+                    setup(gn, Gn);
+                    start(Gn);
+                }
+            }
+            for (uint32_t k = 1; k <= K; k += 2) {
+                step(k, ae, 0);                                // odd k: line k+1 goes to slot 0
+                if (k == K)
+                    break;
+                step(k + 1, ao, 1);                            // even k: line k+1 goes to slot 1
+            }
+            // padding, digest (md5.c:134-168): the lane's own tail length
+            if (t == 0) {
+                Alg::pad_only(st, G.len);
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < 16; i++) {
+                    const uint32_t o = 4 * i;
+                    const uint32_t keep = t > o ? (t - o < 4 ? t - o : 4) : 0;
+                    uint32_t v = keep == 4 ? wt[i] : wt[i] & ((1u << (8 * keep)) - 1u);
+                    if (t >= o && t < o + 4)
+                        v |= 0x80u << (8 * (t - o));
+                    wt[i] = v;
+                }
+                Alg::finish(st, wt, t, G.len);
+            }
+        }
+        if (r < n_rec)
+            Alg::template store<OUT_ALIGNED>(out, r, st);
+        g = gn;
+        if (g >= n_groups)
+            break;
+        G = Gn;
+    }
+}
+
+// One 8-wave workgroup per CU (128 KiB of LDS), groups handed out by tickets.
+template <class Alg>
+hipError_t launch_var_line(const uint8_t *data, const uint64_t *offs, const uint32_t *lens, uint64_t n_rec, uint8_t *out,
+                           bool out_al, hipStream_t s)
+{
+    constexpr int W = 8;
+    const uint64_t groups = (n_rec + 63) / 64;
+    const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
+    if (out_al)
+        digest_var_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, offs, lens, n_rec, out);
+    else
+        digest_var_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, offs, lens, n_rec, out);
+    return hipGetLastError();
+}
+
+// BRB_TEST_VAR_LINE=0 keeps variable-length batches on the per-lane kernel (A/B measurements).
+inline bool var_line_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("BRB_TEST_VAR_LINE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+}  // namespace brb_digest

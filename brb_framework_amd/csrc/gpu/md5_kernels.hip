@@ -7,6 +7,7 @@
 #include "brb_kernels.h"
 #include "byte_stream.h"
 #include "digest_dma.h"
+#include "digest_var_line.h"
 #include "md5_device.h"
 
 namespace {
@@ -140,6 +141,9 @@ hipError_t launch_md5_var(const uint8_t *data, const uint64_t *offs, const uint3
     if (n_rec == 0)
         return hipSuccess;
     const bool out_al = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    // line-aligned LDS-DMA staging (digest_var_line.h); the per-lane kernel below is its A/B baseline
+    if (brb_digest::var_line_enabled())
+        return brb_digest::launch_var_line<Md5Alg>(data, offs, lens, n_rec, out, out_al, s);
     const unsigned g = grid_for(n_rec);
     if (out_al)
         md5_any_kernel<kBlock, false, true><<<g, kBlock, 0, s>>>(data, offs, lens, 0, n_rec, out);

@@ -323,3 +323,48 @@ def test_concurrent_host_threads(brb, orc, torch_dev):
         th.join(timeout=100)
     assert not errors, errors
     assert len(results) == 24 and all(a and b for a, b in results.values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,max_len,seed", [(70_001, 3000, 1), (5_000, 200, 2), (3_000, 20_000, 3)])
+def test_variable_records_line_kernel(brb, orc, torch_dev, n, max_len, seed):
+    """BRB_MD5Batch / BrbSha1_Batch through the line-staged variable-length kernel
+    (digest_var_line.h): every byte alignment, overlapping records, empty records, groups whose
+    records differ in length by up to max_len; host, device and all-devices modes vs the oracle."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[rng.integers(0, n, n // 20)] = 0
+    span = int(lens.astype(np.uint64).sum() // 2 + max_len + 64)
+    offs = rng.integers(0, span - max_len, n).astype(np.uint64)          # overlapping, any byte
+    buf = workload.gen_records(0x5EED0011 + seed, 0, 1, span)
+    want5, want1 = orc.md5_batch(buf, offs, lens), orc.sha1_batch(buf, offs, lens)
+    assert np.array_equal(brb.md5_batch(buf, offs, lens), want5)
+    assert np.array_equal(brb.sha1_batch(buf, offs, lens), want1)
+    d, o, ln = to_dev(torch_dev, buf), to_dev(torch_dev, offs.view(np.int64)), to_dev(torch_dev, lens.view(np.int32))
+    assert np.array_equal(brb.md5_batch(d, o, ln).cpu().numpy(), want5)
+    assert np.array_equal(brb.sha1_batch(d, o, ln).cpu().numpy(), want1)
+    assert np.array_equal(brb.md5_batch(buf, offs, lens, all_devices=True), want5)
+
+
+@pytest.mark.gpu
+def test_variable_records_wide_span(brb, orc, torch_dev):
+    """Groups whose records lie more than 2 GiB apart (32-bit DMA offsets cannot reach them) are
+    digested by the per-lane path inside the same launch; the other groups stay line-staged."""
+    far = (1 << 31) + 12345
+    n = 640
+    rng = np.random.default_rng(12)
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    offs = rng.integers(0, 1 << 20, n).astype(np.uint64)
+    offs[::7] += far                                                     # every group spans > 2 GiB
+    offs[128:192] = rng.integers(0, 1 << 20, 64).astype(np.uint64)       # one group does not
+    d = torch_dev.empty(far + (1 << 20) + 4096, dtype=torch_dev.uint8, device="cuda")
+    lo_h = workload.gen_records(0x5EED0012, 0, 1, (1 << 20) + 4096)
+    hi_h = workload.gen_records(0x5EED0013, 0, 1, (1 << 20) + 4096)
+    d[: lo_h.size] = to_dev(torch_dev, lo_h)
+    d[far: far + hi_h.size] = to_dev(torch_dev, hi_h)
+    got5 = brb.md5_batch(d, to_dev(torch_dev, offs.view(np.int64)), to_dev(torch_dev, lens.view(np.int32))).cpu().numpy()
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        src = hi_h[o - far: o - far + L] if o >= far else lo_h[o: o + L]
+        assert got5[i].tobytes() == hashlib.md5(src.tobytes()).digest(), i
+    del d
