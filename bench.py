@@ -57,6 +57,7 @@ def parse():
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B); "
                          "metadata / base64: f4 on the same shape")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
+    ap.add_argument("--rec-len", type=int, default=0, help="override the record length of a digest config")
     ap.add_argument("--streams", type=int, default=1, help="HIP streams the timed steps alternate over")
     ap.add_argument("--two-stream", action="store_true", help="also time the steps over 2 streams")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -283,7 +284,7 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     import brb_framework_amd as brb
     from brb_framework_amd import workload
 
-    L = cfg["rec_len"]
+    L = args.rec_len or cfg["rec_len"]
     if cfg_id == 5:
         n_rank = workload.CONFIGS[5]["records"] // 8          # one GPU's shard of cfg5
     else:
@@ -368,7 +369,8 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "dtype": "u32",
         "data": "synthetic (SURVEY §8(d) splitmix64 generator, HBM-resident, L3-defeating rotation of "
                 f"{n_rot} copies)",
-        "config": {"workload": cfg["name"] + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else "")
+        "config": {"workload": (cfg["name"] if not args.rec_len else f"{n_rank} x {L} B records (cfg{cfg_id} shape, --rec-len)")
+                   + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else "")
                    + (f"; the same batch on each of {world} GPUs" if world > 1 and cfg_id != 5 else ""),
                    "op": f"{'BRB_MD5BatchFixed' if args.op == 'md5' else 'BrbSha1_BatchFixed'} (device mode)",
                    "records_per_gpu": n_rank, "record_bytes": L, "global_records": n_global,
@@ -391,7 +393,7 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, log)
     del bufs, outs
     torch.cuda.empty_cache()
-    if cfg_id == 2 and args.op == "md5" and not args.no_cfg5 and not args.records_per_gpu:
+    if cfg_id == 2 and args.op == "md5" and not args.no_cfg5 and not args.records_per_gpu and not args.rec_len:
         result["cfg5"] = bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_digest(args, host, L, n_rank, log)

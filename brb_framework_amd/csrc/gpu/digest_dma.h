@@ -11,6 +11,7 @@
 #pragma once
 
 #include "digest_line.h"
+#include "digest_var_line.h"
 #include "dma_stage.h"
 
 namespace brb_digest {
@@ -191,6 +192,16 @@ inline bool dma_supported(uint32_t rec_len)
     return rec_len > 0 && uint64_t(rec_len) * 64 + 64 < (uint64_t(1) << 31);
 }
 
+// BRB_TEST_FIXED_VAR_LINE=0 keeps byte-aligned fixed-stride records on the record-relative kernel.
+inline bool fixed_var_line_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("BRB_TEST_FIXED_VAR_LINE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <class Alg>
 hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
                             hipStream_t s)
@@ -208,6 +219,8 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
     // cfg2: 25.3 -> 24.9 us (tools/mb/md5_ab.hip).
     if (line_supported(data, rec_len))
         return launch_fixed_line<Alg>(data, rec_len, n_rec, out, out_al, s);
+    if (rec_len > 64 && rec_len <= (1u << 20) && fixed_var_line_enabled())
+        return launch_fixed_var_line<Alg>(data, rec_len, n_rec, out, out_al, s);   // any byte alignment
     if (rec_len > 64) {
         // one 8-wave workgroup per CU (two waves per SIMD, 128 KiB of LDS), persistent, groups
         // handed out by tickets, 128-byte stages, ring of 2

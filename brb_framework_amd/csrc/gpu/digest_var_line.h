@@ -65,11 +65,14 @@ BRB_DEV uint64_t wave_max64(uint64_t v)
     return v;
 }
 
-template <class Alg, int WAVES, bool OUT_ALIGNED>
+// FIXED: record r = data[r * rec_len .. + rec_len) (offs / lens unused) -- fixed-stride batches
+// whose records are not 4-byte aligned, which digest_line_kernel's dword window cannot take.
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool FIXED = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const uint8_t *__restrict__ data,
                                                                         const uint64_t *__restrict__ offs,
                                                                         const uint32_t *__restrict__ lens,
-                                                                        uint64_t n_rec, uint8_t *__restrict__ out)
+                                                                        uint32_t rec_len, uint64_t n_rec,
+                                                                        uint8_t *__restrict__ out)
 {
     constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
     constexpr uint32_t OOB = 0x80000000u;                      // a voffset past every descriptor's range
@@ -110,8 +113,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
         const uint64_t r0 = g * 64;
         const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
         const uint64_t r = r0 + (lane < last ? lane : last);
-        G.a = dbase + offs[r];
-        G.len = lens[r];
+        G.a = dbase + (FIXED ? r * rec_len : offs[r]);
+        G.len = FIXED ? rec_len : lens[r];
         const uint64_t line = G.a & ~uint64_t(127);
         const uint32_t lines = G.len ? uint32_t(((G.a & 127) + G.len + 127) >> 7) : 0u;
         const uint32_t nblk = (G.len >> 6) + ((G.len & 63) ? 1u : 0u);
@@ -297,9 +300,23 @@ hipError_t launch_var_line(const uint8_t *data, const uint64_t *offs, const uint
     const uint64_t groups = (n_rec + 63) / 64;
     const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
     if (out_al)
-        digest_var_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, offs, lens, n_rec, out);
+        digest_var_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
     else
-        digest_var_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, offs, lens, n_rec, out);
+        digest_var_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
+    return hipGetLastError();
+}
+
+template <class Alg>
+hipError_t launch_fixed_var_line(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
+                                 hipStream_t s)
+{
+    constexpr int W = 8;
+    const uint64_t groups = (n_rec + 63) / 64;
+    const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
+    if (out_al)
+        digest_var_line_kernel<Alg, W, true, true><<<g, 64 * W, 0, s>>>(data, nullptr, nullptr, rec_len, n_rec, out);
+    else
+        digest_var_line_kernel<Alg, W, false, true><<<g, 64 * W, 0, s>>>(data, nullptr, nullptr, rec_len, n_rec, out);
     return hipGetLastError();
 }
 
