@@ -247,6 +247,20 @@ int digest_part(brb_host::FixedLauncher launch, size_t dig, const uint8_t *data,
     if (!ws)
         return fail_hip("device workspace", e);
     const uint64_t per = L ? std::max<uint64_t>(1, digest_chunk_bytes() / L) : n;
+    if (per >= n) {
+        // one chunk: nothing to overlap, so no worker hand-off and no events -- H2D, kernel and D2H
+        // in order on one stream (tools/call_latency.cpp: the pipeline's machinery cost ~48 us per
+        // call on batches of 1..1024 records)
+        if (L && (e = hipMemcpyAsync(ws, data, n * L, hipMemcpyHostToDevice, p->s_k)) != hipSuccess)
+            return drain(p, fail_hip("hipMemcpyAsync H2D", e));
+        if ((e = launch(ws, L, n, ws + off_out, p->s_k)) != hipSuccess)
+            return drain(p, fail_hip("kernel launch", e));
+        if ((e = hipMemcpyAsync(digests, ws + off_out, dig * n, hipMemcpyDeviceToHost, p->s_k)) != hipSuccess)
+            return drain(p, fail_hip("hipMemcpyAsync D2H", e));
+        if ((e = hipStreamSynchronize(p->s_k)) != hipSuccess)
+            return drain(p, fail_hip("hipStreamSynchronize", e));
+        return BRB_BATCH_OK;
+    }
     Pending pending;
     int rc = BRB_BATCH_OK;
     uint64_t c = 0;
@@ -291,9 +305,18 @@ int blowfish_part(const BRB_BLOWFISH_CTX *ctx, uint64_t *words, uint64_t nb, boo
         return fail_hip("device workspace", e);
     const uint64_t *dctx = reinterpret_cast<const uint64_t *>(ws);
     uint64_t *dw = reinterpret_cast<uint64_t *>(ws + ctx_bytes);
+    const uint64_t per = std::max<uint64_t>(1, chunk_bytes() / 16);
+    if (per >= nb) {                                           // one chunk: one stream, one sync
+        if ((e = hipMemcpyAsync(ws, ctx, sizeof(BRB_BLOWFISH_CTX), hipMemcpyHostToDevice, p->s_k)) != hipSuccess ||
+            (e = hipMemcpyAsync(dw, words, 16 * nb, hipMemcpyHostToDevice, p->s_k)) != hipSuccess ||
+            (e = brb::launch_blowfish(dctx, dw, nb, decrypt, p->s_k)) != hipSuccess ||
+            (e = hipMemcpyAsync(words, dw, 16 * nb, hipMemcpyDeviceToHost, p->s_k)) != hipSuccess ||
+            (e = hipStreamSynchronize(p->s_k)) != hipSuccess)
+            return drain(p, fail_hip("single-chunk Blowfish batch", e));
+        return BRB_BATCH_OK;
+    }
     if ((e = hipMemcpyAsync(ws, ctx, sizeof(BRB_BLOWFISH_CTX), hipMemcpyHostToDevice, p->s_in)) != hipSuccess)
         return drain(p, fail_hip("hipMemcpyAsync H2D", e));
-    const uint64_t per = std::max<uint64_t>(1, chunk_bytes() / 16);
     Pending pending;
     int rc = BRB_BATCH_OK;
     uint64_t c = 0;
