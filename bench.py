@@ -411,19 +411,38 @@ def host_rate(call, nbytes, reps=5):
     return {"gib_s": round(nbytes / dt / 2**30, 2), "gb_s": round(nbytes / dt / 1e9, 2), "ms": round(dt * 1e3, 3)}
 
 
+def registered_copy(arr):
+    """A copy of `arr` in page-aligned host memory page-locked with BRB_CryptoGPU_HostRegister (what a
+    C caller does with its own buffers); returns (region, numpy view).  Delete the view, then
+    region.close()."""
+    import numpy as np
+
+    import brb_framework_amd as brb
+    reg = brb.crypto.HostRegion(arr.nbytes)
+    view = np.frombuffer(reg._mm, np.uint8, count=arr.nbytes).view(arr.dtype).reshape(arr.shape)
+    view[...] = arr
+    return reg, view
+
+
 def bench_pcie_digest(fn, host, L, n, width, log):
     """Host-inclusive rate through the C ABI's host mode (input in host memory, digests back in host
     memory, the call returns when they are there): pageable input (a plain numpy array, what a
-    receive loop's calloc'd buffers are) and page-locked input (torch pin_memory)."""
+    receive loop's calloc'd buffers are), page-locked input (the same bytes in a region the library
+    page-locked, BRB_CryptoGPU_HostRegister) and torch.pin_memory() input for comparison."""
     import numpy as np
     import torch
     out = np.empty((n, width), np.uint8)
     pageable = host_rate(lambda: fn(host, L, n, out=out), host.nbytes)
-    pinned_t = torch.from_numpy(host).pin_memory()
-    hp = pinned_t.numpy()
+    reg, hp = registered_copy(host)
     pinned = host_rate(lambda: fn(hp, L, n, out=out), host.nbytes)
-    log(f"[bench] host-inclusive: pageable {pageable['gb_s']} GB/s, pinned {pinned['gb_s']} GB/s")
+    del hp
+    reg.close()
+    tp = torch.from_numpy(host).pin_memory().numpy()
+    pinned_torch = host_rate(lambda: fn(tp, L, n, out=out), host.nbytes)
+    log(f"[bench] host-inclusive: pageable {pageable['gb_s']} GB/s, page-locked {pinned['gb_s']} GB/s, "
+        f"torch-pinned {pinned_torch['gb_s']} GB/s")
     return {"gib_s": pageable["gib_s"], "ms_per_batch": pageable["ms"], "pageable": pageable, "pinned": pinned,
+            "pinned_torch": pinned_torch,
             "note": "host-mode call: 32 MiB chunks of whole records copied H2D straight from the caller's memory, overlapped "
                     "with the kernels, digests D2H per chunk; gib_s = pageable input"}
 
@@ -630,10 +649,11 @@ def bench_pcie_blowfish(ctx, w, log):
         brb.blowfish_decrypt_batch(ctx, b)
 
     pageable = host_rate(lambda: trip(buf), w.nbytes, reps=3)
-    pin_t = torch.from_numpy(buf.view("int64")).pin_memory()
-    pb = pin_t.numpy().view("uint64")
+    reg, pb = registered_copy(buf)
     pinned = host_rate(lambda: trip(pb), w.nbytes, reps=3)
     assert (pb == w).all() and (buf == w).all(), "host-mode round trip did not restore the plaintext"
+    del pb
+    reg.close()
     log(f"[bench] cfg4 host-inclusive: pageable {pageable['gib_s']} GiB/s, pinned {pinned['gib_s']} GiB/s")
     return {"gib_s": pageable["gib_s"], "ms_per_round_trip": pageable["ms"], "pageable": pageable, "pinned": pinned,
             "note": "two host-mode calls (encrypt, decrypt) over the 1 GiB in place: 16 MiB chunks, H2D on the calling "
