@@ -127,11 +127,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // bytes left), so every voffset stays >= 1024 whatever the record length or group size: one DMA
     // form for every group, no per-DMA M0 writes.
     uint32_t vq[8], vqn[8];                                    // this group's, the next group's
-    // Descriptor of the next line to issue: base = that line - 4096, num_records = 4096 + bytes from
-    // the line to end_line, clamped to [0, 2^31 - 1].  Set once per group (dma_setup) and advanced
-    // by one line per issue with four scalar ops.  A group at least 2^31 - 4097 bytes from the end
-    // starts at 2^31 - 1 and stays above every voffset of its K + 1 lines (line_supported caps
-    // rec_len at 1 MiB: voffsets < 64 MiB + 8 KiB).
+    // Descriptor of a group: base = the group's first line - 4096, num_records = 4096 + bytes from
+    // that line to end_line, clamped to [0, 2^31 - 1].  Set once per group (dma_setup); line j of
+    // the group is addressed by soffset = 128 j, one scalar add per issue (round 3: the per-line
+    // descriptor advance took four scalar ops plus hipcc's copies).  A group at least 2^31 - 4097
+    // bytes from the end has num_records 2^31 - 1, above every offset of its K + 1 lines
+    // (line_supported caps rec_len at 1 MiB: offsets < 64 MiB + 8 KiB).
     brb_dma::v4i rs, rsn;
     // The next group's offsets and descriptor go to vqn / rsn (taken over once per group): written
     // into vq / rs inside the loop, they made hipcc copy all eight offsets on every iteration.
@@ -158,42 +159,37 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             vq[q] = (((x < cap ? x : cap) & ~127u) | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
         }
     };
-    auto issue = [&](const uint32_t (&vq)[8], brb_dma::v4i &rs, uint32_t slot) {   // next line -> slot
+    // soffset of the next line to issue (the descriptor stays put for the whole group; the range
+    // check covers voffset + soffset + the instruction offset, per dword: tools/mb/buf_range.hip).
+    uint32_t so = 0, son = 0;
+    auto issue = [&](const uint32_t (&vq)[8], const brb_dma::v4i &rs, uint32_t &so, uint32_t slot) {   // next line -> slot
         const uint32_t m = lds0 + slot * SLOT;
         uint32_t keep;
 #define BRB_LINE_DMA8(POL)                                                                      \
     asm volatile("s_mov_b32 %0, m0\n\t"                                                          \
                  "s_mov_b32 m0, %10\n\t"                                                         \
                  "s_nop 0\n\t"                                                                   \
-                 "buffer_load_dwordx4 %1, %9, 0 offen " POL "lds\n\t"                            \
-                 "buffer_load_dwordx4 %2, %9, 0 offen offset:1024 " POL "lds\n\t"                \
-                 "buffer_load_dwordx4 %3, %9, 0 offen offset:2048 " POL "lds\n\t"                \
-                 "buffer_load_dwordx4 %4, %9, 0 offen offset:3072 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %1, %9, %12 offen " POL "lds\n\t"                         \
+                 "buffer_load_dwordx4 %2, %9, %12 offen offset:1024 " POL "lds\n\t"             \
+                 "buffer_load_dwordx4 %3, %9, %12 offen offset:2048 " POL "lds\n\t"             \
+                 "buffer_load_dwordx4 %4, %9, %12 offen offset:3072 " POL "lds\n\t"             \
                  "s_mov_b32 m0, %11\n\t"                                                         \
                  "s_nop 0\n\t"                                                                   \
-                 "buffer_load_dwordx4 %5, %9, 0 offen " POL "lds\n\t"                            \
-                 "buffer_load_dwordx4 %6, %9, 0 offen offset:1024 " POL "lds\n\t"                \
-                 "buffer_load_dwordx4 %7, %9, 0 offen offset:2048 " POL "lds\n\t"                \
-                 "buffer_load_dwordx4 %8, %9, 0 offen offset:3072 " POL "lds\n\t"                \
+                 "buffer_load_dwordx4 %5, %9, %12 offen " POL "lds\n\t"                         \
+                 "buffer_load_dwordx4 %6, %9, %12 offen offset:1024 " POL "lds\n\t"             \
+                 "buffer_load_dwordx4 %7, %9, %12 offen offset:2048 " POL "lds\n\t"             \
+                 "buffer_load_dwordx4 %8, %9, %12 offen offset:3072 " POL "lds\n\t"             \
                  "s_mov_b32 m0, %0"                                                               \
                  : "=&s"(keep)                                                                    \
                  : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "v"(vq[4]), "v"(vq[5]), "v"(vq[6]), \
-                   "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u)                                    \
+                   "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u), "s"(so)                           \
                  : "memory")
         if constexpr (NT)
             BRB_LINE_DMA8("nt ");
         else
             BRB_LINE_DMA8("");
 #undef BRB_LINE_DMA8
-        // rs: the line after the issued one.  base += 128 with carry; num_records = max(nr - 128, 0)
-        // in scalar asm (hipcc lowers the saturating subtract to v_sub ... clamp, which moves the
-        // whole descriptor into VGPRs).
-        const uint64_t b = ((uint64_t(uint32_t(rs.y)) << 32) | uint32_t(rs.x)) + 128u;
-        rs.x = int(uint32_t(b));
-        rs.y = int(uint32_t(b >> 32));
-        int z = rs.z;
-        asm("s_sub_i32 %0, %0, 0x80\n\ts_max_i32 %0, %0, 0" : "+s"(z) : : "scc");
-        rs.z = z;
+        so += 128;                                             // the line after the issued one
     };
 
     // ---- read side: window dword i of this lane -> LDS offset, for lines (k-1, k) in slots
@@ -233,8 +229,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     BRB_LINE_PROBE_DECL
     BRB_LINE_PROBE(0);
     dma_setup(g, vq, rs);
-    issue(vq, rs, 0);
-    issue(vq, rs, 1);
+    issue(vq, rs, so, 0);
+    issue(vq, rs, so, 1);
     // Everything else of the prologue runs while the first two lines are in flight: without the
     // barrier hipcc hoisted the window tables (~300 VALU) above the first DMA.
     __builtin_amdgcn_sched_barrier(0);
@@ -244,36 +240,54 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     tail_masks(t, tm, tp);
     // One iteration k (1 <= k <= K): wait for line k, read the window (lines k-1, k), refill the
     // slot of line k-1 with line k+1 (at k = K: start the next group's lines 0 and 1), hash blocks
-    // 2k-2 and 2k-1.  Unrolled by two so that each parity reads with its own address table; the
-    // loop thus holds four compress sites (the shared instruction cache holds them: unrolling the
-    // whole record did not fit).
-    auto step = [&](typename Alg::State &st, uint32_t k, const uint32_t (&ad)[32], uint32_t refill_slot) {
+    // 2k-2 and 2k-1.  Iterations k < K always refill and always hash two whole blocks
+    // (2k - 1 <= 2K - 3 < nfull), so they run branch-free in a loop unrolled by two (each parity
+    // reads with its own address table: four compress sites, which the shared instruction cache
+    // holds; unrolling the whole record did not fit).  The last iteration is peeled:
+    // it alone starts the next group and checks which blocks are whole.  Round 3: the peeled form
+    // issues ~18 fewer scalar/branch instructions per iteration than one loop with the checks.
+    auto full_step = [&](typename Alg::State &st, const uint32_t (&ad)[32], uint32_t refill_slot) {
         BRB_LINE_PROBE(1);
         brb_dma::wait_vmcnt<0>();
         read_window(ad);
         BRB_LINE_PROBE(2);
-        if (k < K) {
-            issue(vq, rs, refill_slot);
-        } else if (gn < n_groups) {
-            dma_setup(gn, vqn, rsn);
-            issue(vqn, rsn, 0);
-            issue(vqn, rsn, 1);
-        }
-        const uint32_t b = 2 * k - 2;
-        if (b < nfull)
-            Alg::compress(st, w0);
-        if (b + 1 < nfull)
-            Alg::compress(st, w1);
+        issue(vq, rs, so, refill_slot);
+        // Without branches between the steps hipcc interleaved the compressions with the window
+        // reads (one s_waitcnt per dword) and hoisted the next window read above them.
+        __builtin_amdgcn_sched_barrier(0);
+        Alg::compress(st, w0);
+        Alg::compress(st, w1);
+        __builtin_amdgcn_sched_barrier(0);
     };
     for (;;) {
         typename Alg::State st = Alg::iv();
-        for (uint32_t k = 1;; k += 2) {
-            step(st, k, ae, 0);                                // odd k: line k+1 goes to slot 0
-            if (k == K)
-                break;
-            step(st, k + 1, ao, 1);                            // even k: line k+1 goes to slot 1
-            if (k + 1 == K)
-                break;
+        uint32_t k = 1;
+        for (; k + 2 <= K; k += 2) {
+            full_step(st, ae, 0);                              // odd k: line k+1 goes to slot 0
+            full_step(st, ao, 1);                              // even k: line k+1 goes to slot 1
+        }
+        if (k < K) {                                           // K even: iteration K-1 (odd) is left
+            full_step(st, ae, 0);
+        }
+        {   // iteration K: the window table of its parity, selected once per group
+            uint32_t al[32];
+#pragma unroll
+            for (int i = 0; i < 32; i++)
+                al[i] = (K & 1) ? ae[i] : ao[i];
+            BRB_LINE_PROBE(1);
+            brb_dma::wait_vmcnt<0>();
+            read_window(al);
+            BRB_LINE_PROBE(2);
+            if (gn < n_groups) {
+                dma_setup(gn, vqn, rsn);
+                son = 0;
+                issue(vqn, rsn, son, 0);
+                issue(vqn, rsn, son, 1);
+            }
+            if (2 * K - 2 < nfull)
+                Alg::compress(st, w0);
+            if (2 * K - 1 < nfull)
+                Alg::compress(st, w1);
         }
         line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
         g = gn;
@@ -284,6 +298,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         for (int q = 0; q < 8; q++)
             vq[q] = vqn[q];
         rs = rsn;
+        so = son;
         win_setup(g);
     }
     BRB_LINE_PROBE(3);
