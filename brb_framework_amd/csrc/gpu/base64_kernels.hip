@@ -21,6 +21,19 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kWaves = kBlock / 64;
+constexpr uint32_t kXch = 4096;                 // per-wave exchange of the cooperative loads / stores
+
+// Wave-uniform maximum (loop bounds of the cooperative loads and stores).
+BRB_DEV uint32_t wave_max(uint32_t x)
+{
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = uint32_t(__shfl_xor(int(x), o));
+        x = y > x ? y : x;
+    }
+    return __builtin_amdgcn_readfirstlane(x);
+}
 
 BRB_DEV uint32_t alpha(uint32_t i)   // base64.c:42
 {
@@ -79,81 +92,51 @@ __global__ __launch_bounds__(kBlock) void b64_encode_kernel(const uint8_t *__res
                                                             const uint64_t *__restrict__ ooffs)
 {
     __shared__ uint16_t pair[4096];
+    __shared__ __attribute__((aligned(16))) uint8_t xin[kWaves * kXch], xout[kWaves * kXch];
     for (uint32_t e = threadIdx.x; e < 4096; e += kBlock)
         pair[e] = uint16_t(alpha(e >> 6) | (alpha(e & 63) << 8));
     __syncthreads();
     const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n)
-        return;
-    const uint64_t len = lens[r];
+    const bool live = r < n;                      // lanes past n only take part in the wave's loads/stores
+    const uint64_t len = live ? lens[r] : 0;
     const uint64_t olen = 4 * ((len + 2) / 3);
-    brb_io::BlockSrc src;
-    brb_io::Snk snk;
-    src.init(in + offs[r], len);
-    snk.init(out + ooffs[r], olen);
-    uint32_t a[16], b[16], c[16], o[16];
-    const uint64_t steps = len / 192;
-    for (uint64_t st = 0; st < steps; st++) {
-        src.fetch(a);
-        src.fetch(b);
-        src.fetch(c);
-        encode16<0>(pair, a, b, c, o);
-        snk.put16(o);
-        encode16<1>(pair, a, b, c, o);
-        snk.put16(o);
-        encode16<2>(pair, a, b, c, o);
-        snk.put16(o);
-        encode16<3>(pair, a, b, c, o);
-        snk.put16(o);
+    const uint32_t wv = threadIdx.x >> 6;
+    brb_io::StepSrcW<3> src;
+    brb_io::SnkW snk;
+    src.init(in + (live ? offs[r] : 0), len, xin + wv * kXch);
+    snk.init(out + (live ? ooffs[r] : 0), olen, xout + wv * kXch);
+    // step st: input bytes [192 st, 192 st + 192) -> characters [256 st, 256 st + 256) = output
+    // blocks 4 st .. 4 st + 3; the last step of a record holds its 0..191-byte tail
+    const uint64_t full = len / 192;
+    const uint32_t t = uint32_t(len - 192 * full);            // 0..191 tail bytes (zeros past them)
+    const uint32_t qfull = t / 3, rest = t % 3;               // quantum qfull holds the 1- or 2-byte tail
+    const uint32_t nloop = wave_max(uint32_t(full + (t ? 1 : 0)));
+    uint32_t blk[3][16], o[4][16];
+    if (nloop) {
+        src.issue(0);
+        src.take(blk);
     }
-    const uint32_t t = uint32_t(len - 192 * steps);           // 0..191 tail bytes (zeros past them)
-    if (t) {
-        src.fetch(a);
-        if (t > 64)
-            src.fetch(b);
-        else
-#pragma unroll
-            for (int i = 0; i < 16; i++)
-                b[i] = 0;
-        if (t > 128)
-            src.fetch(c);
-        else
-#pragma unroll
-            for (int i = 0; i < 16; i++)
-                c[i] = 0;
-        const uint32_t full = t / 3, rest = t % 3;            // quantum `full` holds the 1- or 2-byte tail
+    for (uint32_t st = 0; st < nloop; st++) {
+        if (st + 1 < nloop)
+            src.issue(st + 1);                                // in flight while step st is encoded
+        const bool in_full = st < full, in_tail = st == full && t;
         // the padding rule of base64.c:335-352 (bytes past the record read as 0 above)
         auto pad = [&](uint32_t v, uint32_t u) {
-            return u == full && rest ? (rest == 1 ? (v & 0x0000FFFFu) | 0x3D3D0000u : (v & 0x00FFFFFFu) | 0x3D000000u) : v;
+            return in_tail && u == qfull && rest ? (rest == 1 ? (v & 0x0000FFFFu) | 0x3D3D0000u : (v & 0x00FFFFFFu) | 0x3D000000u) : v;
         };
-        encode16<0>(pair, a, b, c, o);
+#define BRB_ENC(H)                                                                          \
+        encode16<H>(pair, blk[0], blk[1], blk[2], o[H]);                                    \
+        _Pragma("unroll") for (int k = 0; k < 16; k++) o[H][k] = pad(o[H][k], 16 * H + k);
+        BRB_ENC(0) BRB_ENC(1) BRB_ENC(2) BRB_ENC(3)
+#undef BRB_ENC
+        if (st + 1 < nloop)
+            src.take(blk);                                    // before this step's stores (StepSrcW)
 #pragma unroll
-        for (int k = 0; k < 16; k++)
-            o[k] = pad(o[k], k);
-        snk.put16(o);                                         // Snk writes no byte past olen
-        if (t > 48) {
-            encode16<1>(pair, a, b, c, o);
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                o[k] = pad(o[k], 16 + k);
-            snk.put16(o);
-        }
-        if (t > 96) {
-            encode16<2>(pair, a, b, c, o);
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                o[k] = pad(o[k], 32 + k);
-            snk.put16(o);
-        }
-        if (t > 144) {
-            encode16<3>(pair, a, b, c, o);
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                o[k] = pad(o[k], 48 + k);
-            snk.put16(o);
-        }
+        for (int h = 0; h < 4; h++)
+            snk.put16(o[h], 4 * st + h, in_full || (in_tail && t > 48u * h));
     }
-    snk.flush();
+    if (live)
+        snk.flush();                                          // Snk writes no byte past olen
 }
 
 // base64.c:363-376: alphabet value, 0 for '=', -1 for anything else (NUL included)
@@ -182,21 +165,27 @@ BRB_DEV uint32_t group3(const int8_t *val, uint32_t ch)
     return s | (uint32_t(v0 | v1 | v2 | v3) & 0x80000000u);
 }
 
-// 16 groups (one 64-character block) -> 12 output dwords at o[12 k ..]; returns the OR of the flags
-BRB_DEV uint32_t decode_block(const int8_t *val, const uint32_t (&c)[16], uint32_t (&o)[48], int k)
+// 16 groups (one 64-character block) -> 12 output dwords at o[12 k ..]; flag word q (bit 31 set: a
+// character outside the alphabet / '=') covers groups 4q .. 4q + 3, one bit 31 per group in
+// bits 31, 30, 29, 28 so that a partial step can ignore the groups past its end (group_mask)
+BRB_DEV void decode_block4(const int8_t *val, const uint32_t (&c)[16], uint32_t (&o)[48], int k, uint32_t (&f)[4])
 {
-    uint32_t bad = 0;
 #pragma unroll
     for (int g = 0; g < 16; g += 4) {
         const uint32_t s0 = group3(val, c[g]), s1 = group3(val, c[g + 1]), s2 = group3(val, c[g + 2]),
                        s3 = group3(val, c[g + 3]);
-        bad |= s0 | s1 | s2 | s3;
+        f[g / 4] = (s0 & 0x80000000u) | ((s1 >> 1) & 0x40000000u) | ((s2 >> 2) & 0x20000000u) | ((s3 >> 3) & 0x10000000u);
         const int q = 12 * k + 3 * (g / 4);
         o[q] = (s0 & 0xFFFFFFu) | (s1 << 24);
         o[q + 1] = ((s1 & 0xFFFFFFu) >> 8) | (s2 << 16);
         o[q + 2] = ((s2 & 0xFFFFFFu) >> 16) | (s3 << 8);
     }
-    return bad;
+}
+
+// flags of the first m (>= 1) groups of a flag word, folded onto bit 31
+BRB_DEV uint32_t group_mask(uint32_t m)
+{
+    return m >= 4 ? 0xF0000000u : (0xF0000000u << (4 - m)) & 0xF0000000u;
 }
 
 __global__ __launch_bounds__(kBlock) void b64_decode_kernel(const uint8_t *__restrict__ in,
@@ -207,56 +196,87 @@ __global__ __launch_bounds__(kBlock) void b64_decode_kernel(const uint8_t *__res
                                                             uint32_t *__restrict__ olens)
 {
     __shared__ int8_t val[256];
+    __shared__ __attribute__((aligned(16))) uint8_t xin[kWaves * kXch], xout[kWaves * kXch];
     for (uint32_t e = threadIdx.x; e < 256; e += kBlock)
         val[e] = int8_t(b64_value(e));
     __syncthreads();
     const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n)
-        return;
-    const uint64_t len = lens[r];
-    const uint8_t *a = in + offs[r];
-    brb_io::Snk snk;
-    snk.init(out + ooffs[r], 3 * (len / 4));
+    const bool live = r < n;                      // lanes past n only take part in the wave's loads/stores
+    const uint64_t len = live ? lens[r] : 0;
+    const uint8_t *a = in + (live ? offs[r] : 0);
+    const uint32_t wv = threadIdx.x >> 6;
+    brb_io::SnkW snk;
+    snk.init(out + (live ? ooffs[r] : 0), 3 * (len / 4), xout + wv * kXch);
+    // Steps of 256 characters (4 input blocks -> 64 groups -> 3 output blocks) in one wave-uniform
+    // loop.  A lane's last step may be partial: its whole groups decode the same way and a trailing
+    // partial group is dropped (base64.c:171-175).  At the first step whose whole groups hold a byte
+    // outside the alphabet / '=' (a skipped byte or a NUL), the lane leaves the loop's output and
+    // finishes with the reference's character-serial rules from that step's start.
     uint64_t pos = 0;
     uint32_t produced = 0;
-    if (len >= 256) {
-        // steps of 256 characters while every one of them is in the alphabet or '=': 64 whole groups
-        brb_io::BlockSrc src;
-        src.init(a, len);
-        uint32_t c0[16], c1[16], c2[16], c3[16], o[48];
-        for (; pos + 256 <= len; pos += 256) {
-            src.fetch(c0);
-            src.fetch(c1);
-            src.fetch(c2);
-            src.fetch(c3);
-            const uint32_t bad = decode_block(val, c0, o, 0) | decode_block(val, c1, o, 1) |
-                                 decode_block(val, c2, o, 2) | decode_block(val, c3, o, 3);
-            if (bad & 0x80000000u)
-                break;                                        // skipped bytes or a NUL: serial from pos
-            uint32_t h[16];
+    bool fast = true;
+    {
+        brb_io::StepSrcW<4> src;
+        src.init(a, len, xin + wv * kXch);
+        const uint32_t nloop = wave_max(uint32_t((len + 255) / 256));
+        uint32_t c[4][16], o[48];
+        if (nloop) {
+            src.issue(0);
+            src.take(c);
+        }
+        for (uint32_t st = 0; st < nloop; st++) {
+            if (st + 1 < nloop)
+                src.issue(st + 1);
+            const uint64_t p0 = 256ull * st;
+            const uint32_t nch = fast && p0 < len ? uint32_t(len - p0 < 256 ? len - p0 : 256) : 0u;
+            const uint32_t ng = nch / 4;                          // whole groups of this step
+            uint32_t bad = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t b4[4];
+                decode_block4(val, c[k], o, k, b4);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    bad |= 16u * k + 4u * q < ng ? b4[q] & group_mask(ng - 16u * k - 4u * q) : 0u;
+            }
+            const bool act = nch && !bad;
+            if (nch && !act) {
+                fast = false;                                     // serial from this step's start
+                pos = p0;
+            }
+            if (act) {
+                pos = p0 + nch;
+                produced += 3 * ng;
+            }
+            if (st + 1 < nloop)
+                src.take(c);
 #pragma unroll
             for (int q = 0; q < 3; q++) {
+                uint32_t h[16];
 #pragma unroll
                 for (int i = 0; i < 16; i++)
                     h[i] = o[16 * q + i];
-                snk.put16(h);
+                snk.put16(h, 3 * st + q, act && 3 * ng > 64u * q);
             }
-            produced += 192;
         }
     }
-    // base64.c:131-179, character by character, from pos (a group boundary: val = cnt = 0)
+    if (!live)
+        return;
+    // base64.c:131-179, character by character, from pos (a group boundary: val = cnt = 0); after
+    // the fast loop only a lane that met a skipped byte or a NUL, or a trailing partial group, is left
+    brb_io::Snk &ss = snk.s;
     brb_io::Src src;
     src.init(a + pos, len - pos);
     uint32_t val4 = 0, cnt = 0, outn = 0;
     uint64_t outacc = 0;
-    bool live = true;
-    for (uint64_t c4 = pos; c4 < len && live; c4 += 4) {
+    bool on = !fast;
+    for (uint64_t c4 = pos; c4 < len && on; c4 += 4) {
         const uint32_t chunk = src.next();
         const uint32_t nb = len - c4 >= 4 ? 4u : uint32_t(len - c4);
         for (uint32_t b = 0; b < nb; b++) {
             const uint32_t ch = (chunk >> (8 * b)) & 0xFFu;
             if (ch == 0) {              // C-string end (base64.c:146)
-                live = false;
+                on = false;
                 break;
             }
             const int v = val[ch];
@@ -271,17 +291,17 @@ __global__ __launch_bounds__(kBlock) void b64_decode_kernel(const uint8_t *__res
             produced += 3;
             val4 = cnt = 0;
             if (outn >= 4) {
-                snk.put(uint32_t(outacc));
+                ss.put(uint32_t(outacc));
                 outacc >>= 32;
                 outn -= 4;
             }
         }
     }
     if (outn) {
-        snk.rem = outn;
-        snk.put(uint32_t(outacc));
+        ss.rem = outn;
+        ss.put(uint32_t(outacc));
     }
-    snk.flush();
+    ss.flush();
     olens[r] = produced;
 }
 

@@ -367,3 +367,51 @@ def test_rc4_sector_sink_ragged(brb):
     r = subprocess.run([sys.executable, "-c", _SECTOR_SCRIPT, root], env=dict(os.environ, BRB_TEST_RC4_SECTOR="1"),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "sector sink ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_rc4_ragged_out_of_place(brb, orc):
+    """Ragged, packed streams (0..3000 B, the block-edge lengths first) at every input byte offset,
+    in place and out of place into an output buffer shifted so that output and input alignments
+    differ; device mode, against the oracle, states included; bytes between streams untouched."""
+    import torch
+    rng = np.random.default_rng(11)
+    for base in (0, 1, 2, 3):
+        for shift in (None, 0, 1, 5, 37, 63):
+            lens = rng.integers(0, 3000, 257).astype(np.uint32)
+            lens[:8] = [0, 1, 63, 64, 65, 127, 128, 129]
+            gaps = rng.integers(0, 6, 257)
+            offs = (base + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64) + gaps[:-1])])).astype(np.uint64)
+            total = int(offs[-1] + lens[-1]) + 8
+            data = workload.gen_records(0x5EED00A1, base, 1, total)
+            keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(len(offs))]
+            states = brb.rc4_states(keys)
+            want = data.copy()
+            want_st = states.copy()
+            for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+                s2, ob = orc.rc4_crypt(states[i].tobytes(), data[o:o + n].tobytes())
+                want[o:o + n] = np.frombuffer(ob, np.uint8)
+                want_st[i] = np.frombuffer(s2, np.uint8)
+            t = torch.from_numpy(data).cuda()
+            st = torch.from_numpy(states).cuda()
+            if shift is None:
+                brb.rc4_crypt_batch(st, t, torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda())
+                got = t.cpu().numpy()
+            else:
+                fill = np.full(total + 64, 0xA5, np.uint8)
+                big = torch.from_numpy(fill).cuda()
+                out = big[shift:shift + total]
+                brb.rc4_crypt_batch(st, t, torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda(), out=out)
+                got = out.cpu().numpy()
+                # bytes outside the streams stay untouched
+                want = np.where(_covered(offs, lens, total), want, np.uint8(0xA5))
+                assert np.array_equal(big.cpu().numpy()[:shift], fill[:shift])
+            assert np.array_equal(got, want), (base, shift)
+            assert np.array_equal(st.cpu().numpy(), want_st), (base, shift)
+
+
+def _covered(offs, lens, total):
+    m = np.zeros(total, bool)
+    for o, n in zip(offs.tolist(), lens.tolist()):
+        m[o:o + n] = True
+    return m
