@@ -24,7 +24,7 @@ def main():
         json.dump(lines, fo, indent=1, sort_keys=True)
         fo.write("\n")
     for k, v in lines.items():
-        r = v.get("roofline", {})
+        r = v.get("roofline") or {}
         print(f"{k:10s} {v.get('value')} {v.get('unit')}  frac {r.get('frac')}  us {r.get('launch_us_avg', r.get('step_us_avg'))}")
 
 
