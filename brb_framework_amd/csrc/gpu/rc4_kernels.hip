@@ -37,7 +37,7 @@ BRB_DEV uint32_t wave_max(uint32_t x)
 
 // BlockSrcW exchange per wave.  Only the plain RC4 pass loads cooperatively: 65 536 x 1500 B,
 // 135 -> 124 us.  The frame and open kernels, whose MD5 work per block hides the per-lane loads,
-// measured slower with it (frame 141 -> 150 us, open 139 -> 143 us, rocprofv3, tools/gpu_ab_lib.sh).
+// measured slower with it (frame 141 -> 150 us, open 139 -> 143 us, rocprofv3, tools/gpu_ab_prof.sh).
 constexpr uint32_t kXchBytes = 4096;
 
 // Decrypt frame block b (chunks 16b .. 16b + 15 of a frame of F bytes, fetched into c) into pt and
