@@ -38,36 +38,37 @@ struct Perm {
     BRB_DEV void wr(uint32_t x, uint32_t v) const { lds[addr(x)] = uint8_t(v); }
 };
 
-// Keystream generator: BRB_RC4_Crypt's index1/index2 walk (rc4.c:71-82), software-pipelined so that
-// no LDS round trip sits on the byte-to-byte dependency chain.
+// Keystream generator: BRB_RC4_Crypt's index1/index2 walk (rc4.c:71-82), software-pipelined.
 //
 // The serial form of byte t is  i += 1; a = S[i]; j += a; b = S[j]; S[i] = b; S[j] = a;
-// k = S[a + b].  Its chain is j -> S[j] (an LDS read) -> the swap writes -> the next byte's S[j']
-// read, which must see them.  Here the next byte's reads are issued BEFORE the current byte's swap
-// is written, and the values are patched with the swaps they missed:
-//   * step() STARTS byte T+1 (a, j, and the raw read of S[j]) and then COMPLETES byte T (patch
-//     S[j_T], write its swap, read k_T).  The raw S[j_T] was read before swap T-1 was written:
-//     b_T = j_T == j_{T-1} ? a_{T-1} : j_T == i_{T-1} ? b_{T-1} : raw.
-//   * S[i] is read two bytes ahead (positions i+1, i+2 in flight); a raw S[i_{T+1}] missed swaps
-//     T-2, T-1 and T, and since i_s != i_{T+1} for those, only j_s == i_{T+1} -> a_s applies.
+// k = S[a + b].  step() STARTS byte T+1 (a, j, the S[j] address) and then COMPLETES byte T (write
+// its swap, read S[j_{T+1}] and k_T):
+//   * S[j_{T+1}] is read right after swap T is written, so it is exact: the one LDS write -> read
+//     round trip per byte on the chain is covered by the rest of the step;
+//   * S[i] is read two bytes ahead (positions i+1, i+2 in flight), before the swap of its step is
+//     written; a raw S[i_{T+1}] missed swaps T-2, T-1 and T, and since i_s != i_{T+1} for those,
+//     only j_s == i_{T+1} -> a_s applies (three compare/select pairs).
 // So j_{T+1} = j_T + a_{T+1} is pure VALU.  Indices are kept as running 32-bit sums (2^32 is a
 // multiple of 256); an LDS address is one v_perm_b32 of the sum's low byte and the lane's column,
-// and the patches compare addresses, so no masking op is needed anywhere (16 VALU per byte).
+// and the patches compare addresses, so no masking op is needed anywhere.
 // Before the first byte the "previous swaps" are identity swaps (S[ci] = S[ci], S[cj] = S[cj]),
 // which patch nothing wrongly, so there is no special case.  One byte is always started ahead of
 // the last one returned; store() drops it (its swap was never written), so the state advances by
 // exactly the bytes returned.
-// Measured (65 536 streams x 1500 B, MI355X): 188 us serial form -> 170 us; hand-scheduled inline
-// asm variants with one and two steps of read-ahead ran 178 and 195 us: at one wave per SIMD the
-// kernel is bound by instruction issue (~30 per byte) with the LDS queue of the 4 waves behind it.
+// Measured (65 536 streams x 1500 B, MI355X): 188 us serial form -> 170 us pipelined with S[j]
+// read before swap T and patched (two more pairs); hand-scheduled inline asm variants with one and
+// two steps of read-ahead ran 178 and 195 us.  Round 3, interleaved A/B (rocprofv3 means): reading
+// S[j] after the swap instead of patching it took the RC4 pass 123.0 -> 117.4 us, the frame kernel
+// 141.2 -> 130.0 us and the open kernel 138.1 -> 124.7 us; moving the S[i] read after the swap too
+// (one pair fewer) ran 128 us: the read then lands too late for the step that needs it.
 struct Gen {
     Perm P;
     // Every index is kept as (running 32-bit sum, LDS address).  Two indices are equal mod 256 iff
     // their addresses are (same lane column), so all compares are on addresses.
     // started byte T: j (sum), S[i_T], raw S[j_T], addresses of S[i_T] and S[j_T]
     uint32_t j, a, rb, ai, aj;
-    // swap T-1 (written): addresses of i and j, a, b; swap T-2: address of j, a
-    uint32_t pai, paj, pa, pb, qaj, qa;
+    // swap T-1 (written): addresses of i and j, a; swap T-2: address of j, a
+    uint32_t pai, paj, pa, qaj, qa;
     // S[i] read ahead: positions i_T + 1 and i_T + 2 (running sums), raw values, addresses
     uint32_t p1, r1, ad1, p2, r2, ad2;
     uint32_t tail;     // dword 64 of the state: index1, index2 and the two bytes after them
@@ -92,7 +93,6 @@ struct Gen {
         const uint32_t ci = tail & 255u, cj = (tail >> 8) & 255u;
         pai = ad(ci);                  // identity swaps before byte 0: S[ci] = S[ci], S[cj] = S[cj]
         paj = ad(cj);
-        pb = rd(pai);
         pa = rd(paj);
         qaj = paj;
         qa = pa;
@@ -123,22 +123,20 @@ struct Gen {
     BRB_DEV uint32_t step()
     {
         // ---- start byte T+1 at position p1
-        uint32_t a1 = r1;
+        uint32_t a1 = r1;                    // read before swap T-2 was written
         a1 = qaj == ad1 ? qa : a1;           // swap T-2
         a1 = paj == ad1 ? pa : a1;           // swap T-1
         a1 = aj == ad1 ? a : a1;             // swap T (not written yet)
         const uint32_t j1 = j + a1;
         const uint32_t aj1 = ad(j1);
-        const uint32_t rb1 = rd(aj1);        // sees swaps <= T-1
         const uint32_t p3 = p2 + 1;
         const uint32_t ad3 = ad(p3);
         const uint32_t r3 = rd(ad3);         // S[i_{T+1} + 2], sees swaps <= T-1
         // ---- complete byte T
-        uint32_t b = rb;                     // read before swap T-1 was written
-        b = aj == pai ? pb : b;
-        b = aj == paj ? pa : b;
+        const uint32_t b = rb;               // S[j_T], read after swap T-1 was written: exact
         wr(ai, b);                           // S[i] = S[j]
         wr(aj, a);                           // S[j] = S[i]   (rc4.c:76-78)
+        const uint32_t rb1 = rd(aj1);        // S[j_{T+1}] after swap T: exact
         const uint32_t k = rd(ad(a + b));    // S[S[i] + S[j]]
         // ---- shift the pipeline
         qaj = paj;
@@ -146,7 +144,6 @@ struct Gen {
         pai = ai;
         paj = aj;
         pa = a;
-        pb = b;
         j = j1;
         a = a1;
         rb = rb1;
