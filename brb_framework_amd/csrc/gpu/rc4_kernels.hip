@@ -73,11 +73,17 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
 }
 
 // SECTOR: outputs through brb_io::SectorSnk (whole aligned 64-byte sectors) instead of Snk.
-// Measured (tools/gpu_rc4_sector.sh, 65 536 x 1500 B, two interleaved rounds): HBM outputs 123.0 ->
-// 128.3 us per pass (the sink's LDS row and address selects add ~50 VALU per block to ~1 100 for the
-// keystream) for 190.9 -> 152.8 MB written; zero-copy batcher rounds (outputs into page-locked host
-// memory over PCIe) 1.87 -> 1.81 ms pipelined, 2.50 -> 2.54 ms one round at a time.  So HBM outputs
-// keep Snk and the zero-copy batcher uses SectorSnk.
+// Measured with the first pipelined generator (tools/gpu_rc4_sector.sh, 65 536 x 1500 B, two
+// interleaved rounds): HBM outputs 123.0 -> 128.3 us per pass (the sink's LDS row and address selects
+// add ~50 VALU per block to ~1 100 for the keystream) for 190.9 -> 152.8 MB written; zero-copy batcher
+// rounds (outputs into page-locked host memory over PCIe) 1.87 -> 1.81 ms pipelined.  With the
+// round-3 generator (S[j] read after the swap, rc4_device.h), whose steps wait on LDS as much as on
+// issue, the sink's extra VALU fit in those waits: HBM outputs 120.9 -> 118.2 us (three interleaved
+// rounds, tools/gpu_ab_env.sh BRB_TEST_RC4_SECTOR 0 1) and 187 -> 152 MB written (PMC WRITE_SIZE), so
+// every RC4 pass output now takes SectorSnk.  The open kernel, whose MD5 work already fills those
+// waits, measured slower with it (125.4 -> 134.9 us, interleaved, a build with these kernels templated on
+// the sink; not kept), so the frame and
+// open kernels keep Snk.
 template <bool SECTOR>
 __global__ __launch_bounds__(kWave) void rc4_crypt_kernel(uint8_t *__restrict__ states, const uint8_t *in, uint8_t *out,
                                                           const uint64_t *__restrict__ offs,
@@ -323,7 +329,7 @@ hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, co
 {
     if (n == 0)
         return hipSuccess;
-    // BRB_TEST_RC4_SECTOR=0/1 forces the sink for A/B measurements (tools/gpu_rc4_sector.sh)
+    // BRB_TEST_RC4_SECTOR=0/1 forces the sink for A/B measurements (tools/gpu_ab_env.sh)
     static const int force = [] {
         const char *e = getenv("BRB_TEST_RC4_SECTOR");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
