@@ -60,6 +60,36 @@ struct Funnel {
         acc = x >> 32;
     }
 
+    // Word-aligned input (metadata_unpack_kernel): the caller reads the next piece starting nacc
+    // bytes early, so its words fall on MD5 word boundaries; the low nacc bytes of its first word
+    // are replaced by the carried bytes (head), whole words go straight to the ring (put16w,
+    // put_tail), and the bytes of a last partial word become the carry.  `total` is the caller's.
+    BRB_DEV uint32_t head(uint32_t w0) const
+    {
+        return nacc ? (w0 & ~((1u << (8 * nacc)) - 1u)) | uint32_t(acc) : w0;
+    }
+    BRB_DEV void put16w(const uint32_t (&w)[16])
+    {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            word(w[i]);
+    }
+    // the first `left` (< 64) bytes of w: whole words to the ring, the rest (zeros past it) carried
+    BRB_DEV void put_tail(const uint32_t (&w)[16], uint32_t left)
+    {
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++)
+            if (4 * i + 4 <= left)
+                word(w[i]);
+        const uint32_t k = left >> 2;
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; i++)
+            t = i == k ? w[i] : t;
+        nacc = left & 3;
+        acc = nacc ? t : 0u;
+    }
+
     BRB_DEV void load16(uint32_t (&w)[16]) const
     {
 #pragma unroll

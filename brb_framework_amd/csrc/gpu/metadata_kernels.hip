@@ -107,25 +107,31 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
             // is hashed; the data comes in 64-byte blocks with the next one in flight
             Ahead<7> nx;
             nx.issue(base, size, offset + sz);
-            const uint64_t avail = offset < size ? (sz < size - offset ? sz : size - offset) : 0;
+            // The data is read from e = (bytes digested so far) mod 4 bytes before it (the item's
+            // own fields, offset >= 88 > e), so its words fall on the digest's word boundaries: one
+            // funnel shift per word (in BlockSrc) and no carry shifting (md5_funnel.h put16w); the
+            // first word's e low bytes are the carried ones.  Here sz + 1 <= size - offset.
+            const uint32_t e = f.nacc;
+            const uint64_t n = sz + e;
             brb_io::BlockSrc bs;   // two blocks in flight (registers copied per block): 75.7 -> 81.4 us
-            bs.init(base + (offset < size ? offset : 0), avail);
-            for (uint64_t c = 0; c < sz; c += 64) {         // :249-254 BRB_MD5UpdateBig of the data
+            bs.init(base + offset - e, n);
+            for (uint64_t c = 0; c < n; c += 64) {          // :249-254 BRB_MD5UpdateBig of the data
                 uint32_t w[16];
                 bs.fetch(w);
-                const uint64_t left = sz - c;
-                if (left >= 64) {
-#pragma unroll
-                    for (int k = 0; k < 16; k++)
-                        f.put4(w[k]);
-                } else {
-#pragma unroll
-                    for (uint32_t k = 0; k < 16; k++)
-                        if (4 * k < left)
-                            f.put(w[k], left - 4 * k >= 4 ? 4u : uint32_t(left - 4 * k));
-                }
+                if (c == 0)
+                    w[0] = f.head(w[0]);
+                const uint64_t left = n - c;
+                if (left >= 64)
+                    f.put16w(w);
+                else
+                    f.put_tail(w, uint32_t(left));
                 f.pump();
             }
+            if ((n & 63) == 0) {                            // ended on a whole block: nothing carried
+                f.acc = 0;
+                f.nacc = 0;
+            }
+            f.total += sz;
             offset += sz;
             remaining -= sz;
             if ((nx.dw(0) & 0xFFu) != 0x1Fu) {              // :258-268
