@@ -1,8 +1,8 @@
 """GPU parity: the HIP batch kernels (through the C ABI) against the CPU oracle, bit for bit.
 
 Small cases run the oracle on every record; full BASELINE sizes are checked against the oracle on
-all records where it finishes in seconds (cfg2, cfg3) and through size-independent properties
-where it does not (cfg4: sampled records vs the oracle + exact decrypt(encrypt(x)) == x).
+all records where it finishes in seconds (cfg2, cfg3, cfg4's 1 GiB, cfg5's 1 Mi-record shard) plus
+size-independent properties (cfg4: exact decrypt(encrypt(x)) == x).
 """
 import hashlib
 
@@ -248,8 +248,9 @@ def test_blowfish_golden_cfg4_prefix(brb, torch_dev, golden):
 
 
 def test_cfg4_full_round_trip(brb, orc, torch_dev):
-    """cfg4 at full size (65 536 x 16 KiB = 1 GiB): sampled records == oracle, and the exact
-    64-bit round trip restores every word."""
+    """cfg4 at full size (65 536 x 16 KiB = 1 GiB): every ciphertext word == the 16-thread oracle
+    (all 64 bits, the reference's carries included), and the exact 64-bit round trip restores every
+    word."""
     cfg = workload.CONFIGS[4]
     n_words = cfg["records"] * cfg["rec_len"] // 8
     torch = torch_dev
@@ -259,10 +260,9 @@ def test_cfg4_full_round_trip(brb, orc, torch_dev):
     d = to_dev(torch, w.view(np.int64))
     cd = torch.frombuffer(bytearray(brb.blowfish_ctx_bytes(ctx)), dtype=torch.uint8).cuda()
     brb.blowfish_encrypt_batch(cd, d)
-    wpr = cfg["rec_len"] // 8
-    for r in list(np.random.default_rng(4).integers(0, cfg["records"], 48)) + [0, cfg["records"] - 1]:
-        got = d[r * wpr:(r + 1) * wpr].cpu().numpy().view(np.uint64)
-        assert np.array_equal(got, orc.bf_ecb(oc, w[r * wpr:(r + 1) * wpr].copy())), r
+    want = orc.bf_ecb(oc, w.copy(), threads=16)
+    assert np.array_equal(d.cpu().numpy().view(np.uint64), want)
+    del want
     brb.blowfish_decrypt_batch(cd, d)
     assert torch.equal(d, to_dev(torch, w.view(np.int64)))
 
