@@ -84,3 +84,23 @@ def test_batch_past_4gib(brb, torch_dev, rec_len):
         rec = host[r * rec_len:(r + 1) * rec_len].tobytes()
         assert got[r].tobytes() == hashlib.md5(rec).digest(), f"md5 record {r}"
         assert got1[r].tobytes() == hashlib.sha1(rec).digest(), f"sha1 record {r}"
+
+
+def test_random_record_shapes(brb, orc, torch_dev):
+    """A seeded sweep of 48 record shapes: lengths from 1 B to 12 KiB (so their residues mod 128,
+    which set the line kernel's window shifts, and mod 4, which pick the kernel, vary), base offsets
+    0..15 and batch sizes around the 64-record group; device mode against the oracle on every
+    record, MD5 and SHA-1."""
+    rng = np.random.default_rng(0x5EED0031)
+    for case in range(48):
+        rec_len = int(rng.integers(1, 12289)) if case % 3 else int(rng.integers(65, 400))
+        n = int(rng.choice([1, 63, 64, 65, 127, 129, 300]))
+        off = int(rng.integers(0, 16))
+        data = workload.gen_records(0x5EED0040 + case, 0, n, rec_len)
+        d = torch_dev.zeros(off + data.size + 8, dtype=torch_dev.uint8, device="cuda")
+        d[off:off + data.size] = torch_dev.from_numpy(data).cuda()
+        view = d[off:off + data.size]
+        assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(),
+                              orc.md5_batch_fixed(data, rec_len, n, threads=8)), (case, rec_len, n, off)
+        assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
+                              orc.sha1_batch_fixed(data, rec_len, n, threads=8)), (case, rec_len, n, off)
