@@ -53,7 +53,7 @@ def parse():
                          "ramped up before the timed region)")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--op", default="md5", choices=["md5", "sha1", "md5var", "sha1var", "rc4", "rc4md5", "batcher",
-                                                  "metadata", "base64"],
+                                                  "metadata", "md5seg", "base64"],
                     help="rc4 / rc4md5: SURVEY §8 f1 on the cfg2 shape (65 536 connections x 1500 B); "
                          "metadata / base64: f4 on the same shape")
     ap.add_argument("--records-per-gpu", type=int, default=0, help="override the per-GPU record count")
@@ -204,7 +204,7 @@ def main():
         result = bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif args.op in ("md5var", "sha1var"):
         result = bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log)
-    elif args.op in ("metadata", "base64"):
+    elif args.op in ("metadata", "md5seg", "base64"):
         result = bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     elif cfg["op"] == "blowfish":
         result = bench_blowfish(args, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
@@ -891,6 +891,9 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
     """SURVEY §8 f4 on the cfg2 shape (65 536 records of 1500 data bytes per GPU, HBM-resident).
     --op metadata: one step = BRB_MetaDataUnpackBatch over 65 536 MetaData packs of 4 items x 375 B
                    (1 664 bytes each: header, item headers, data, canaries), every pack valid.
+    --op md5seg:   one step = BRB_MD5BatchSegments over the same packs' items (MetaDataHeaderLoadData,
+                   meta_data.c:397-433: MD5 of a MetaData's 4 item ranges), checked against the
+                   digests the packs carry.
     --op base64:   one step = BRB_Base64EncodeBatch of the 1500-byte records (2000 characters each),
                    then BRB_Base64DecodeBatch of those texts back into 1500-byte records."""
     import numpy as np
@@ -905,7 +908,7 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
     host = workload.gen_records(workload.SEEDS[2], rank * n, n, L)
     Lb = brb.lib()
     flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
-    if args.op == "metadata":
+    if args.op in ("metadata", "md5seg"):
         K, Q = 4, L // 4                         # items per pack, bytes per item
         P_SZ = 64 + K * (24 + Q + 1)
         packs = np.zeros((n, P_SZ), np.uint8)
@@ -932,11 +935,25 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         bptr = [b.data_ptr() for b in bufs]
         po, pl, pi = offs.data_ptr(), lens.data_ptr(), info.data_ptr()
 
-        def launch(k, s, j=0):
-            if Lb.BRB_MetaDataUnpackBatch(bptr[k % n_rot], po, pl, n, pi, flags, s.cuda_stream) != 1:
-                raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
-        moved, payload, name = n * (P_SZ + 32), n * P_SZ, "BRB_MetaDataUnpackBatch"
-        metric = "GiB/s of MetaData packs validated (MetaDataUnpack: walk, canaries, MD5) (SURVEY §8 f4)"
+        if args.op == "metadata":
+            def launch(k, s, j=0):
+                if Lb.BRB_MetaDataUnpackBatch(bptr[k % n_rot], po, pl, n, pi, flags, s.cuda_stream) != 1:
+                    raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+            moved, payload, name = n * (P_SZ + 32), n * P_SZ, "BRB_MetaDataUnpackBatch"
+            metric = "GiB/s of MetaData packs validated (MetaDataUnpack: walk, canaries, MD5) (SURVEY §8 f4)"
+        else:
+            item0 = np.array([64 + j * (24 + Q + 1) + 24 for j in range(K)], np.uint64)
+            soffs = torch.from_numpy((offs_h[:, None] + item0[None, :]).reshape(-1).view(np.int64)).to(dev)
+            slens = torch.full((n * K,), Q, dtype=torch.int32, device=dev)
+            sfirst = torch.from_numpy((np.arange(n + 1, dtype=np.uint64) * K).view(np.int64)).to(dev)
+            digs = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+            so, sl, sf, pd = soffs.data_ptr(), slens.data_ptr(), sfirst.data_ptr(), digs.data_ptr()
+
+            def launch(k, s, j=0):
+                if Lb.BRB_MD5BatchSegments(bptr[k % n_rot], so, sl, sf, n, pd, flags, s.cuda_stream) != 1:
+                    raise RuntimeError(Lb.BRB_CryptoGPU_LastError().decode())
+            moved, payload, name = n * (K * Q + 16), n * K * Q, "BRB_MD5BatchSegments"
+            metric = "GiB/s of MetaData item bytes digested (MetaDataHeaderLoadData: MD5 over a record's segments) (SURVEY §8 f4)"
     else:
         T = 4 * ((L + 2) // 3)
         n_rot = max(2, math.ceil(640e6 / host.nbytes))
@@ -971,6 +988,8 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         got = info.cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
         assert (got["error_code"] == 7).all() and (got["item_count"] == 4).all(), "a pack failed to unpack"
         assert (got["cur_offset"] == P_SZ).all()
+    elif args.op == "md5seg":
+        assert np.array_equal(digs.cpu().numpy(), packs[:, 24:40]), "segment digests differ from the packs' digests"
     else:
         assert (olens.cpu().numpy() == L).all()
         last = (n_warm + n_steps - 1) % n_rot
@@ -997,7 +1016,15 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         th = cpu_threads()
         m = min(n, 16384)
         reps, t0 = 0, time.perf_counter()
-        if args.op == "metadata":
+        if args.op == "md5seg":
+            # the same digests on the CPU: the oracle's MD5 over each record's items, which are the
+            # record's 1500 bytes back to back
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                dg = oracle.md5_batch_fixed(host[: m * L], L, m, threads=th)
+                reps += 1
+            assert np.array_equal(dg, packs[:m, 24:40])
+            cores, sample = th, f"oracle MD5 of {m} records' 4 x {Q} B items (concatenated), {reps} passes, {th} pthreads"
+        elif args.op == "metadata":
             fl = flat[: m * P_SZ]
             while time.perf_counter() - t0 < args.cpu_seconds:
                 inf = oracle.metadata_unpack_batch(fl, offs_h[:m], lens_h[:m], threads=th)
@@ -1013,7 +1040,7 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                 reps += 1
             cores, sample = 1, f"oracle encode + decode of {m} records x {L} B, {reps} passes, 1 thread"
         dt = time.perf_counter() - t0
-        result["cpu_baseline"] = {"value": round(m * L * reps / dt / 2**30, 3) if args.op == "base64"
+        result["cpu_baseline"] = {"value": round(m * L * reps / dt / 2**30, 3) if args.op in ("base64", "md5seg")
                                   else round(m * P_SZ * reps / dt / 2**30, 3), "unit": "GiB/s", "cores": cores,
                                   "kind": "port", "sample": sample}
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per step")

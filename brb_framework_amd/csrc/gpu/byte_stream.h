@@ -274,14 +274,18 @@ struct BlockSrc {
         }
     }
 
-    BRB_DEV void init(const uint8_t *a, uint64_t n)
+    // `lo` (optional): the range's bytes below lo are not memory to read (md5_seg_kernel starts a
+    // segment's range up to 3 bytes early and overwrites those bytes); a first dword wholly below
+    // lo's dword reads as 0.  Only that dword can lie below: load() starts at dword 1.
+    BRB_DEV void init(const uint8_t *a, uint64_t n, const uint8_t *lo = nullptr)
     {
         const uintptr_t ad = reinterpret_cast<uintptr_t>(a);
         p = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
         sh = uint32_t(ad & 3) * 8;
         len = n;
         ndw = n ? ((ad & 3) + n + 3) / 4 : 0;
-        prev = ndw ? ldg(p) : 0u;
+        const bool below = lo && (ad & ~uintptr_t(3)) < (reinterpret_cast<uintptr_t>(lo) & ~uintptr_t(3));
+        prev = ndw && !below ? ldg(p) : 0u;
         nb = 0;
         load(0);
     }

@@ -1,12 +1,13 @@
 // md5_funnel.h -- one lane's streaming MD5 over bytes that arrive in pieces of 1..4 bytes at any
 // message position (BRB_MD5Init, BRB_MD5UpdateBig per piece, BRB_MD5Final: md5.c:38-168).
 //
-// A 64-bit carry holds the 0..3 message bytes left over from the previous piece; whole 32-bit
-// message words go to the lane's private 32-word ring in LDS, word k of lane l at (k * 64 + l) * 4
-// -- every access of lane l hits bank l.  put()/put4() only write words; pump() compresses the
+// A carry holds the 0..3 message bytes left over from the previous piece; whole 32-bit message
+// words go to the lane's private 32-word ring in LDS, word k of lane l at (k * 64 + l) * 4 -- every
+// access of lane l hits bank l.  The callers read each piece from `nacc` bytes before it, so its
+// words already fall on message word boundaries (head/put16w/put_tail below); pump() compresses the
 // oldest 16 once they are there, and must run at least once per 16 words written.  Keeping the
-// compression out of put() leaves one compress site per caller loop: with it inside, a loop of 16
-// unrolled puts inlined 16 copies of the compression (52 KB of code for metadata_unpack_kernel).
+// compression out of the puts leaves one compress site per caller loop: with it inside, a loop of
+// 16 unrolled puts inlined 16 copies of the compression (52 KB of code for metadata_unpack_kernel).
 // Used by md5_seg_kernel (a record's segments) and metadata_unpack_kernel (a pack's items).
 #pragma once
 
@@ -19,7 +20,7 @@ constexpr uint32_t kRingWords = 32;
 struct Funnel {
     uint32_t *bb;       // ring word k of this lane at bb[64 k] (LDS)
     Md5State st;
-    uint64_t acc, total;
+    uint64_t acc, total; // the carried bytes (low nacc bytes), message bytes so far (the caller's)
     uint32_t nacc;      // bytes held in acc (0..3)
     uint32_t wpos;      // words written
     uint32_t cpos;      // words compressed (a multiple of 16)
@@ -36,28 +37,6 @@ struct Funnel {
     {
         bb[64 * (wpos & (kRingWords - 1))] = w;
         ++wpos;
-    }
-
-    // appends the low `nb` (1..4) bytes of v, least significant first
-    BRB_DEV void put(uint32_t v, uint32_t nb)
-    {
-        total += nb;
-        acc |= uint64_t(v) << (8 * nacc);
-        nacc += nb;
-        if (nacc >= 4) {
-            word(uint32_t(acc));
-            acc >>= 32;
-            nacc -= 4;
-        }
-    }
-
-    // appends 4 bytes (always completes a word)
-    BRB_DEV void put4(uint32_t v)
-    {
-        total += 4;
-        const uint64_t x = acc | (uint64_t(v) << (8 * nacc));
-        word(uint32_t(x));
-        acc = x >> 32;
     }
 
     // Word-aligned input (metadata_unpack_kernel): the caller reads the next piece starting nacc

@@ -28,25 +28,34 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
     f.init(&blk[wave][0][lane]);
     const uint64_t k1 = first[r + 1];
     for (uint64_t k = first[r]; k < k1; k++) {         // 64-byte blocks, the next one in flight
+        // The segment is read as a range starting e = (bytes digested so far) mod 4 bytes before
+        // it, so its words fall on the digest's word boundaries (as metadata_unpack_kernel): those
+        // e bytes are the carried ones (Funnel::head), never loaded from below the segment.
         const uint64_t len = slen[k];
+        if (len == 0)                                   // no bytes: its address need not be memory
+            continue;
+        const uint8_t *a = data + soff[k];
+        const uint32_t e = f.nacc;
+        const uint64_t n = len + e;
         brb_io::BlockSrc src;
-        src.init(data + soff[k], len);
-        for (uint64_t c = 0; c < len; c += 64) {
+        src.init(a - e, n, a);
+        for (uint64_t c = 0; c < n; c += 64) {
             uint32_t w[16];
             src.fetch(w);
-            const uint64_t left = len - c;
-            if (left >= 64) {
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    f.put4(w[i]);
-            } else {
-#pragma unroll
-                for (uint32_t i = 0; i < 16; i++)
-                    if (4 * i < left)
-                        f.put(w[i], left - 4 * i >= 4 ? 4u : uint32_t(left - 4 * i));
-            }
+            if (c == 0)
+                w[0] = f.head(w[0]);
+            const uint64_t left = n - c;
+            if (left >= 64)
+                f.put16w(w);
+            else
+                f.put_tail(w, uint32_t(left));
             f.pump();
         }
+        if ((n & 63) == 0) {                            // ended on a whole block: nothing carried
+            f.acc = 0;
+            f.nacc = 0;
+        }
+        f.total += len;
     }
     const Md5State st = f.finish();
     const uint4 v = make_uint4(st.a, st.b, st.c, st.d);

@@ -116,6 +116,7 @@ def main():
                                ("pmc_rc4", "f1_rc4", "rc4_crypt_kernel", 1),
                                ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2),
                                ("pmc_md", "f4_metadata", "metadata_unpack", 1),
+                               ("pmc_seg", "f4_md5seg", "md5_seg_kernel", 1),
                                ("pmc_b64", "f4_base64", "b64_", 2)):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):

@@ -12,6 +12,7 @@ timeout -k 10 300 python bench.py --config 4 > "$OUT/cfg4.json" 2> "$OUT/cfg4.er
 timeout -k 10 300 python bench.py --op rc4 > "$OUT/rc4.json" 2> "$OUT/rc4.err" && echo "rc4 ok" &&
 timeout -k 10 300 python bench.py --op rc4md5 > "$OUT/rc4md5.json" 2> "$OUT/rc4md5.err" && echo "rc4md5 ok" &&
 timeout -k 10 300 python bench.py --op metadata > "$OUT/metadata.json" 2> "$OUT/metadata.err" && echo "metadata ok" &&
+timeout -k 10 300 python bench.py --op md5seg > "$OUT/md5seg.json" 2> "$OUT/md5seg.err" && echo "md5seg ok" &&
 timeout -k 10 300 python bench.py --op base64 > "$OUT/base64.json" 2> "$OUT/base64.err" && echo "base64 ok" &&
 timeout -k 10 300 python bench.py --op md5var --no-cfg5 > "$OUT/md5var.json" 2> "$OUT/md5var.err" && echo "md5var ok" &&
 timeout -k 10 300 python bench.py --op sha1var --no-cfg5 > "$OUT/sha1var.json" 2> "$OUT/sha1var.err" && echo "sha1var ok" &&

@@ -22,6 +22,7 @@ bash tools/gpu_pmc.sh "${1:-round}/pmc4" --config 4 > /dev/null && echo "pmc4 ok
 bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4" --op rc4 > /dev/null && echo "pmc rc4 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_rc4md5" --op rc4md5 > /dev/null && echo "pmc rc4md5 ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_md" --op metadata > /dev/null && echo "pmc metadata ok" &&
+bash tools/gpu_pmc.sh "${1:-round}/pmc_seg" --op md5seg > /dev/null && echo "pmc md5seg ok" &&
 bash tools/gpu_pmc.sh "${1:-round}/pmc_b64" --op base64 > /dev/null && echo "pmc base64 ok"
 rc=$?
 tail -3 "$OUT/pytest_gpu.log"
