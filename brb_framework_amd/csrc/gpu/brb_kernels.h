@@ -39,7 +39,7 @@ hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint
 // states[sidx ? sidx[i] : i] (sidx: a connection table, the transform batcher's indirection).
 // ooffs: output offsets (nullptr = the input offsets, out mirrors in)
 // sector_out: write whole aligned 64-byte sectors (brb_io::SectorSnk); the default for HBM and host
-// outputs alike since the round-3 generator (rc4_kernels.hip); false = per-stream 16-byte pieces (Snk)
+// outputs alike since the session-4 generator (rc4_kernels.hip); false = per-stream 16-byte pieces (Snk)
 hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, const uint64_t *offs,
                             const uint32_t *lens, uint64_t n, hipStream_t s, const uint32_t *sidx = nullptr,
                             const uint64_t *ooffs = nullptr, bool sector_out = true);

@@ -57,7 +57,7 @@ struct Perm {
 // exactly the bytes returned.
 // Measured (65 536 streams x 1500 B, MI355X): 188 us serial form -> 170 us pipelined with S[j]
 // read before swap T and patched (two more pairs); hand-scheduled inline asm variants with one and
-// two steps of read-ahead ran 178 and 195 us.  Round 3, interleaved A/B (rocprofv3 means): reading
+// two steps of read-ahead ran 178 and 195 us.  Round 2 (session 4), interleaved A/B (rocprofv3): reading
 // S[j] after the swap instead of patching it took the RC4 pass 123.0 -> 117.4 us, the frame kernel
 // 141.2 -> 130.0 us and the open kernel 138.1 -> 124.7 us; moving the S[i] read after the swap too
 // (one pair fewer) ran 128 us: the read then lands too late for the step that needs it.

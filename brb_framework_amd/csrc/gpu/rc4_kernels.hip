@@ -77,7 +77,7 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
 // interleaved rounds): HBM outputs 123.0 -> 128.3 us per pass (the sink's LDS row and address selects
 // add ~50 VALU per block to ~1 100 for the keystream) for 190.9 -> 152.8 MB written; zero-copy batcher
 // rounds (outputs into page-locked host memory over PCIe) 1.87 -> 1.81 ms pipelined.  With the
-// round-3 generator (S[j] read after the swap, rc4_device.h), whose steps wait on LDS as much as on
+// session-4 generator (S[j] read after the swap, rc4_device.h), whose steps wait on LDS as much as on
 // issue, the sink's extra VALU fit in those waits: HBM outputs 120.9 -> 118.2 us (three interleaved
 // rounds, tools/gpu_ab_env.sh BRB_TEST_RC4_SECTOR 0 1) and 187 -> 152 MB written (PMC WRITE_SIZE), so
 // every RC4 pass output now takes SectorSnk.  The open kernel, whose MD5 work already fills those
