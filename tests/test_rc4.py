@@ -356,15 +356,17 @@ print("sector sink ok")
 
 
 @pytest.mark.gpu
-def test_rc4_sector_sink_ragged(brb):
-    """The whole-sector output sink (brb_io::SectorSnk, used by zero-copy batcher rounds) on ragged,
-    packed streams at every byte offset, device mode in place, against the oracle.  The sink is
-    forced with BRB_TEST_RC4_SECTOR=1, which the library reads once per process: one child process."""
+@pytest.mark.parametrize("sector", ["1", "0"])
+def test_rc4_sector_sink_ragged(brb, sector):
+    """Both output sinks of the RC4 pass on ragged, packed streams at every byte offset, device mode
+    in place, against the oracle: brb_io::SectorSnk (whole aligned sectors, the default for every
+    output) and the per-stream Snk it replaced (kept for A/B runs).  The sink is forced with
+    BRB_TEST_RC4_SECTOR, which the library reads once per process: one child process each."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _SECTOR_SCRIPT, root], env=dict(os.environ, BRB_TEST_RC4_SECTOR="1"),
+    r = subprocess.run([sys.executable, "-c", _SECTOR_SCRIPT, root], env=dict(os.environ, BRB_TEST_RC4_SECTOR=sector),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "sector sink ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
