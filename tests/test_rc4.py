@@ -330,6 +330,64 @@ def test_rc4md5_round_trip_large(brb, torch_dev):
         assert fr[fo + 13:fo + 29].tobytes() == hashlib.md5(payload[o:o + m].tobytes()).digest()
 
 
+@pytest.mark.gpu
+def test_rc4_crypt_full_shape(brb, orc, torch_dev):
+    """The f1 bench shape at full size: 65 536 connections x 1500 B through BRB_RC4_CryptBatch (device
+    mode, in place), every stream's output and final state against the oracle's BRB_RC4_Crypt."""
+    torch = torch_dev
+    n, L = 65536, 1500
+    data = workload.gen_records(SEED + 2, 0, n, L)
+    rng = np.random.default_rng(65536)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    states = brb.rc4_states(keys)
+    offs = np.arange(n, dtype=np.uint64) * L
+    lens = np.full(n, L, np.uint32)
+    ts, td = _to(torch, states), _to(torch, data)
+    brb.rc4_crypt_batch(ts, td, _to(torch, offs), _to(torch, lens))
+    got, got_st = td.cpu().numpy(), ts.cpu().numpy()
+    for i in range(n):
+        s2, ob = orc.rc4_crypt(states[i].tobytes(), data[i * L:(i + 1) * L].tobytes())
+        assert got[i * L:(i + 1) * L].tobytes() == ob, i
+        assert got_st[i].tobytes() == s2, i
+
+
+@pytest.mark.gpu
+def test_rc4md5_full_shape(brb, orc, torch_dev):
+    """The rc4md5 bench shape at full size: 65 536 connections x 1500-byte payloads framed on the GPU
+    (BRB_RC4MD5_FrameBatch) equal the oracle's frames and write states byte for byte; opened on the
+    GPU (BRB_RC4MD5_OpenBatch) every frame validates, decrypts to its payload, and the read states
+    equal the oracle's open of the same frames."""
+    torch = torch_dev
+    n, L = 65536, 1500
+    payload = workload.gen_records(SEED + 3, 0, n, L)
+    rng = np.random.default_rng(65537)
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(n)]
+    st0 = brb.rc4_states(keys)
+    offs = np.arange(n, dtype=np.uint64) * L
+    lens = np.full(n, L, np.uint32)
+    F = L + 30
+    foffs = np.arange(n, dtype=np.uint64) * F
+    flens = np.full(n, F, np.uint32)
+    salts = rng.integers(0, 2**32, n, dtype=np.uint64)
+    want_st, want_fr = st0.copy(), np.zeros(n * F, np.uint8)
+    orc.rc4md5_frame_batch(want_st, payload, offs, lens, salts, want_fr, foffs, threads=16)
+    ws, fr = _to(torch, st0), torch.zeros(n * F, dtype=torch.uint8, device="cuda")
+    brb.rc4md5_frame_batch(ws, _to(torch, payload), _to(torch, offs), _to(torch, lens), _to(torch, salts), fr,
+                           _to(torch, foffs))
+    assert np.array_equal(fr.cpu().numpy(), want_fr)
+    assert np.array_equal(ws.cpu().numpy(), want_st)
+    want_rs, want_ok = st0.copy(), np.zeros(n, np.uint8)
+    want_pt = want_fr.copy()
+    orc.rc4md5_open_batch(want_rs, want_pt, foffs, flens, want_ok, threads=16)
+    rs = _to(torch, st0)
+    _, valid = brb.rc4md5_open_batch(rs, fr, _to(torch, foffs), _to(torch, flens))
+    assert int(valid.sum()) == n and want_ok.all()
+    assert np.array_equal(rs.cpu().numpy(), want_rs)
+    got = fr.cpu().numpy().reshape(n, F)
+    assert np.array_equal(got, want_pt.reshape(n, F))
+    assert np.array_equal(got[:, 30:], payload.reshape(n, L))
+
+
 _SECTOR_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, sys.argv[1])
