@@ -136,3 +136,29 @@ def test_decode_falls_back_mid_record(brb, orc):
         assert int(got[i]) == len(w), i
         assert out[int(doffs[i]):int(doffs[i]) + len(w)].tobytes() == w, i
         assert out[int(doffs[i]) + len(w)] == 0xEE, i             # nothing written past the decoded bytes
+
+
+@pytest.mark.gpu
+def test_full_shape_round_trip(brb, torch_dev):
+    """The f4 bench shape at full size: 65 536 records x 1500 B encoded on the GPU equal Python's
+    base64 (RFC 4648) on every record, and decode back to the records (1500 bytes each)."""
+    t = torch_dev
+    n, L = 65536, 1500
+    T = 4 * ((L + 2) // 3)
+    data = workload.gen_records(0x5EED00B6, 0, n, L)
+    offs = np.arange(n, dtype=np.uint64) * L
+    lens = np.full(n, L, np.uint32)
+    toffs = np.arange(n, dtype=np.uint64) * T
+    tlens = np.full(n, T, np.uint32)
+    text = t.zeros(n * T, dtype=t.uint8, device="cuda")
+    brb.base64_encode_batch(t.from_numpy(data).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(), text,
+                            t.from_numpy(toffs).cuda())
+    got = text.cpu().numpy().reshape(n, T)
+    want = np.frombuffer(b"".join(base64.b64encode(data[i * L:(i + 1) * L].tobytes()) for i in range(n)),
+                         np.uint8).reshape(n, T)
+    assert np.array_equal(got, want)
+    back = t.zeros(n * L, dtype=t.uint8, device="cuda")
+    olens = brb.base64_decode_batch(text, t.from_numpy(toffs).cuda(), t.from_numpy(tlens).cuda(), back,
+                                    t.from_numpy(offs).cuda())
+    assert (olens.cpu().numpy() == L).all()
+    assert np.array_equal(back.cpu().numpy(), data)

@@ -174,6 +174,22 @@ def test_unpack_batch_vs_oracle(brb, orc):
 
 
 @pytest.mark.gpu
+def test_unpack_batch_bench_count(brb, orc):
+    """A bench-sized batch: 65 536 valid and mutated packs (every return code) at arbitrary byte
+    offsets, device mode, every BRB_MetaDataUnpackInfo field against the oracle."""
+    import torch
+    packs = corpus(7, 65536)
+    buf, offs, lens = scatter(np.random.default_rng(8), packs)
+    want = [orc.metadata_unpack(p) for p in packs]
+    d = torch.from_numpy(buf).cuda()
+    o = torch.from_numpy(offs.view(np.int64)).cuda()
+    ln = torch.from_numpy(lens.view(np.int32)).cuda()
+    dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    assert infos_as_tuples(dev) == want
+    assert len({w[0] for w in want}) >= 5                     # the corpus reaches the return codes
+
+
+@pytest.mark.gpu
 def test_pack_batch_round_trip(brb, orc):
     from brb_framework_amd import metadata
     rng = np.random.default_rng(5)
