@@ -69,11 +69,13 @@ struct Funnel {
         acc = nacc ? t : 0u;
     }
 
+    // cpos is a multiple of 16, so the 16 words never wrap: one base, immediate offsets
     BRB_DEV void load16(uint32_t (&w)[16]) const
     {
+        const uint32_t *b = bb + 64 * (cpos & 16);
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++)
-            w[i] = bb[64 * ((cpos + i) & (kRingWords - 1))];
+            w[i] = b[64 * i];
     }
 
     BRB_DEV void pump()
