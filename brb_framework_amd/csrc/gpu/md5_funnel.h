@@ -19,23 +19,37 @@ constexpr uint32_t kRingWords = 32;
 
 struct Funnel {
     uint32_t *bb;       // ring word k of this lane at bb[64 k] (LDS)
+    uint32_t ring;      // LDS address of this wave's ring (8 KiB aligned), OR'd into word addresses
+    uint32_t lane4;     // 4 x lane: the lane's byte within a ring row
     Md5State st;
     uint64_t acc, total; // the carried bytes (low nacc bytes), message bytes so far (the caller's)
     uint32_t nacc;      // bytes held in acc (0..3)
     uint32_t wpos;      // words written
     uint32_t cpos;      // words compressed (a multiple of 16)
 
+    // lane_words = &ring[0][lane] of a [32][64] uint32 array at an 8 KiB-aligned LDS address (the
+    // kernels' only __shared__ array), so a word's address is one and-or of its ring offset
     BRB_DEV void init(uint32_t *lane_words)
     {
         bb = lane_words;
+        const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(lane_words));
+        ring = a & ~0x1FFFu;
+        lane4 = a & 0xFFu;
         st = md5_iv();
         acc = total = 0;
         nacc = wpos = cpos = 0;
     }
 
+    static BRB_DEV void lds_st(uint32_t a, uint32_t v) { *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(a) = v; }
+
+    // word at ring position wpos + i (mod 32): (lane4 + 256 (wpos + i)) mod 8 KiB, in the wave's ring
+    BRB_DEV void word_at(uint32_t i, uint32_t w) const
+    {
+        lds_st(((lane4 + ((wpos + i) << 8)) & 0x1FFFu) | ring, w);
+    }
     BRB_DEV void word(uint32_t w)
     {
-        bb[64 * (wpos & (kRingWords - 1))] = w;
+        word_at(0, w);
         ++wpos;
     }
 
@@ -50,8 +64,9 @@ struct Funnel {
     BRB_DEV void put16w(const uint32_t (&w)[16])
     {
 #pragma unroll
-        for (int i = 0; i < 16; i++)
-            word(w[i]);
+        for (uint32_t i = 0; i < 16; i++)
+            word_at(i, w[i]);
+        wpos += 16;
     }
     // the first `left` (< 64) bytes of w: whole words to the ring, the rest (zeros past it) carried
     BRB_DEV void put_tail(const uint32_t (&w)[16], uint32_t left)

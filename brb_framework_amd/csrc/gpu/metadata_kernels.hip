@@ -64,7 +64,7 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
                                                                  const uint32_t *__restrict__ lens, uint64_t n,
                                                                  BRB_MetaDataUnpackInfo *__restrict__ info)
 {
-    __shared__ uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];
+    __shared__ __attribute__((aligned(8192))) uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];   // 8 KiB per wave
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
     if (r >= n)
