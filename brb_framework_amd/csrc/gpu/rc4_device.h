@@ -202,6 +202,18 @@ BRB_DEV uint32_t md5_pad_word(uint32_t raw, uint64_t w, uint64_t len, uint64_t n
     return v;
 }
 
+// Words 16b .. 16b + 15 of the MD5-padded message, in place over the raw words: a block wholly
+// inside the message is its raw words (one compare per block instead of three 64-bit compares and
+// selects per word); only the last one or two blocks take md5_pad_word.
+BRB_DEV void md5_pad_block(uint32_t (&m)[16], uint64_t b, uint64_t len, uint64_t n_words)
+{
+    if (64 * (b + 1) <= len)
+        return;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++)
+        m[i] = md5_pad_word(m[i], 16 * b + i, len, n_words);
+}
+
 // number of 64-byte MD5 blocks of a `len`-byte message including the padding
 BRB_DEV uint64_t md5_blocks(uint64_t len) { return (len + 72) >> 6; }
 

@@ -210,8 +210,9 @@ __global__ __launch_bounds__(kWave) void rc4md5_frame_kernel(uint8_t *__restrict
                     first = raw;
                 ct[i] = __builtin_amdgcn_alignbit(raw, prev, 16) ^ ks[i];
                 prev = raw;
-                m[i] = md5_pad_word(raw, w, len, nw);
+                m[i] = raw;
             }
+            md5_pad_block(m, b, len, nw);
             if (b == 0) {
 #pragma unroll
                 for (int i = 1; i < 16; i++)
@@ -300,8 +301,9 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
             for (int i = 0; i < 16; i++) {
                 const uint32_t lo = i + 7 < 16 ? cur[i + 7] : nxt[i - 9];
                 const uint32_t hi = i + 8 < 16 ? cur[i + 8] : nxt[i - 8];
-                m[i] = md5_pad_word(__builtin_amdgcn_alignbit(hi, lo, 16), 16 * b + i, len, nw);
+                m[i] = __builtin_amdgcn_alignbit(hi, lo, 16);
             }
+            md5_pad_block(m, b, len, nw);
             md5_compress(st, m);
 #pragma unroll
             for (int i = 0; i < 16; i++)
