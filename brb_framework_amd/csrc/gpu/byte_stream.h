@@ -433,6 +433,18 @@ struct StepSrcW {
 
     BRB_DEV void issue(uint64_t st)
     {
+        // the common step: every chunk this lane loads lies inside its range -- NB x 4 plain loads
+        // behind one branch (per-chunk branches cost ~8 instructions per load, AGPR address reads
+        // included, in the base64 kernels)
+        const uint64_t last = 16 * (NB * st + NB - 1) + 4;
+        if (last <= qrem[0] && last <= qrem[1] && last <= qrem[2] && last <= qrem[3]) {
+#pragma unroll
+            for (int j = 0; j < NB; j++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 64 * (NB * st + j)));
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const uint64_t base = 16 * (NB * st + j);
