@@ -443,21 +443,21 @@ struct StepSrcW {
 #pragma unroll
                 for (int q = 0; q < 4; q++)
                     v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 64 * (NB * st + j)));
-            return;
-        }
+        } else {
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-            const uint64_t base = 16 * (NB * st + j);
+            for (int j = 0; j < NB; j++) {
+                const uint64_t base = 16 * (NB * st + j);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (base + 4 <= qrem[q]) {
-                    v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 4 * base));
-                } else {
-                    const uint32_t *d = reinterpret_cast<const uint32_t *>(qa[q]) + base;
-                    v[j][q].x = base + 0 < qrem[q] ? ldg(d + 0) : 0u;
-                    v[j][q].y = base + 1 < qrem[q] ? ldg(d + 1) : 0u;
-                    v[j][q].z = base + 2 < qrem[q] ? ldg(d + 2) : 0u;
-                    v[j][q].w = base + 3 < qrem[q] ? ldg(d + 3) : 0u;
+                for (int q = 0; q < 4; q++) {
+                    if (base + 4 <= qrem[q]) {
+                        v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 4 * base));
+                    } else {
+                        const uint32_t *d = reinterpret_cast<const uint32_t *>(qa[q]) + base;
+                        v[j][q].x = base + 0 < qrem[q] ? ldg(d + 0) : 0u;
+                        v[j][q].y = base + 1 < qrem[q] ? ldg(d + 1) : 0u;
+                        v[j][q].z = base + 2 < qrem[q] ? ldg(d + 2) : 0u;
+                        v[j][q].w = base + 3 < qrem[q] ? ldg(d + 3) : 0u;
+                    }
                 }
             }
         }
