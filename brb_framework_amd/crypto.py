@@ -15,6 +15,8 @@ BATCH_HOST = 0x0
 BATCH_DEVICE = 0x1
 BATCH_ASYNC = 0x2
 BATCH_ALL_DEVICES = 0x4
+BATCH_DROPPED = -2
+TRANSFORM_DROPPED = -1
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 ulp = ctypes.POINTER(ctypes.c_ulong)
@@ -125,6 +127,8 @@ _SIGNATURES = [
     ("BRB_TransformBatcherFlushAsync", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("BRB_TransformBatcherGetState", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(BRB_RC4_State)]),
+    ("BRB_TransformBatcherInjectFault", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("BRB_CryptoGPU_TestOption", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("BRB_CryptoGPU_HostRegister", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
     ("BRB_CryptoGPU_HostUnregister", ctypes.c_int, [ctypes.c_void_p]),
     ("BRB_CryptoGPU_Available", ctypes.c_int, []),
@@ -154,7 +158,9 @@ def lib() -> ctypes.CDLL:
             pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in _SIGNATURES:
-            f = getattr(L, name)
+            f = getattr(L, name, None)
+            if f is None:        # an older build under A/B; tests/test_abi.py checks exports == header
+                continue
             f.restype = res
             f.argtypes = args
         _LIB = L
@@ -168,6 +174,30 @@ def exported_symbols() -> set:
 
 def gpu_available() -> bool:
     return bool(lib().BRB_CryptoGPU_Available())
+
+
+def test_option(name: str, value: int) -> int:
+    """BRB_CryptoGPU_TestOption: sets a process-wide A/B switch, returns its previous value."""
+    old = ctypes.c_int(0)
+    _check(lib().BRB_CryptoGPU_TestOption(name.encode(), int(value), ctypes.byref(old)), "BRB_CryptoGPU_TestOption")
+    return old.value
+
+
+class TestOption:
+    """Context manager: `with TestOption("var_line", 0): ...` restores the previous value on exit."""
+
+    __test__ = False     # not a pytest class
+
+    def __init__(self, name: str, value: int):
+        self.name, self.value, self.old = name, value, None
+
+    def __enter__(self):
+        self.old = test_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        test_option(self.name, self.old)
+        return False
 
 
 def _check(rc: int, what: str) -> None:
@@ -565,6 +595,15 @@ class TransformBatcher:
         fn = TransformDone(cb)
         launched = self._used > 0
         rc = getattr(self._L, fn_name)(self.h, fn, None)
+        if rc == BATCH_DROPPED:
+            # every buffer came back through its callback; those of the dropped round with
+            # valid == TRANSFORM_DROPPED and no output
+            err = RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
+            err.results = res
+            if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
+                self._cur ^= 1
+            self._used = 0
+            raise err
         if rc < 0 or (rc == 0 and self._L.BRB_CryptoGPU_LastError()):
             raise RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
         if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
@@ -579,6 +618,10 @@ class TransformBatcher:
     def flush_async(self):
         """Pipelined: starts this round, returns the previous round's [(conn, op, out, valid)]."""
         return self._run("BRB_TransformBatcherFlushAsync")
+
+    def inject_fault(self, launch: int) -> None:
+        """Test support: the `launch`-th kernel launch of every round fails (-1: off)."""
+        _check(self._L.BRB_TransformBatcherInjectFault(self.h, launch), "BRB_TransformBatcherInjectFault")
 
     def state(self, conn: int, op: int) -> bytes:
         st = BRB_RC4_State()

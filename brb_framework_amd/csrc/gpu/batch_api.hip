@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <mutex>
 #include <cstdio>
@@ -19,6 +20,7 @@
 #include "api_util.h"
 #include "brb_kernels.h"
 #include "host_pipe.h"
+#include "test_options.h"
 
 namespace brb_api {
 
@@ -45,37 +47,42 @@ int fail_hip(const char *what, hipError_t e)
     return BRB_BATCH_NOT_DONE;
 }
 
-// The device count is probed once per process: a batch call from the event loop should not pay a
-// runtime query per call, and the set of visible devices does not change while a process runs.
+// The device count is cached once a probe has found a device: a batch call from the event loop
+// should not pay a runtime query per call, and the set of visible devices does not change while a
+// process runs.  A failed probe is not cached (a transient hipGetDeviceCount error must not disable
+// the library for the rest of the process): the next call probes again.
 namespace {
-std::once_flag g_count_once;
-int g_count = 0;
-std::string g_count_err;
+std::atomic<int> g_count{0};
+std::mutex g_count_mu;
 }  // namespace
 
 int device_count()
 {
-    std::call_once(g_count_once, [] {
-        int n = 0;
-        hipError_t e = hipGetDeviceCount(&n);
-        if (e != hipSuccess) {
-            char buf[256];
-            snprintf(buf, sizeof(buf), "hipGetDeviceCount: %s (%d)", hipGetErrorString(e), int(e));
-            g_count_err = buf;
-            n = 0;
-        } else if (n <= 0) {
-            g_count_err = "no HIP device visible to this process";
-        }
-        g_count = std::max(n, 0);
-    });
-    return g_count;
+    const int n = g_count.load(std::memory_order_acquire);
+    if (n > 0)
+        return n;
+    std::lock_guard<std::mutex> lk(g_count_mu);
+    if (g_count.load(std::memory_order_relaxed) > 0)
+        return g_count.load(std::memory_order_relaxed);
+    int m = 0;
+    if (hipGetDeviceCount(&m) != hipSuccess || m < 0)
+        m = 0;
+    if (m > 0)
+        g_count.store(m, std::memory_order_release);
+    return m;
 }
 
 int device_ok()
 {
     if (device_count() > 0)
         return BRB_BATCH_OK;
-    t_err = g_count_err;
+    int n = 0;
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess)
+        set_err("hipGetDeviceCount: %s (%d)", hipGetErrorString(e), int(e));
+    else
+        set_err("no HIP device visible to this process");
+    (void)hipGetLastError();
     return BRB_BATCH_NOT_DONE;
 }
 
@@ -915,3 +922,33 @@ const char *BRB_CryptoGPU_Version(void)
 }
 
 }  // extern "C"
+
+extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
+{
+    brb_api::clear_err();
+    static const struct {
+        const char *name;
+        brb_opt::Opt opt;
+        int lo, hi;
+    } known[] = {{"rc4_sector", brb_opt::kRc4Sector, -1, 1},
+                 {"var_line", brb_opt::kVarLine, 0, 1},
+                 {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
+                 {"var_sort", brb_opt::kVarSort, 0, 1}};
+    if (!name) {
+        set_err("NULL option name");
+        return BRB_BATCH_BADARG;
+    }
+    for (const auto &k : known)
+        if (strcmp(name, k.name) == 0) {
+            if (value < k.lo || value > k.hi) {
+                set_err("test option %s: value %d out of [%d, %d]", name, value, k.lo, k.hi);
+                return BRB_BATCH_BADARG;
+            }
+            const int prev = brb_opt::g_opt[k.opt].exchange(value, std::memory_order_relaxed);
+            if (old)
+                *old = prev;
+            return BRB_BATCH_OK;
+        }
+    set_err("unknown test option '%s'", name);
+    return BRB_BATCH_BADARG;
+}

@@ -340,6 +340,14 @@ struct BlockSrcW {
     BRB_DEV void issue(uint64_t b)
     {
         const uint64_t base = 16 * b;
+        // the common block: every chunk this lane loads lies inside its range -- four plain loads
+        // behind one branch, as StepSrcW::issue (RC4 pass 118.1 -> 115.4 us)
+        if (base + 4 <= qrem[0] && base + 4 <= qrem[1] && base + 4 <= qrem[2] && base + 4 <= qrem[3]) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                v[q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 4 * base));
+            return;
+        }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (base + 4 <= qrem[q]) {

@@ -192,14 +192,11 @@ inline bool dma_supported(uint32_t rec_len)
     return rec_len > 0 && uint64_t(rec_len) * 64 + 64 < (uint64_t(1) << 31);
 }
 
-// BRB_TEST_FIXED_VAR_LINE=0 keeps byte-aligned fixed-stride records on the record-relative kernel.
+// Test option "fixed_var_line" = 0 keeps byte-aligned fixed-stride records on the record-relative
+// kernel (A/B measurements).
 inline bool fixed_var_line_enabled()
 {
-    static const bool on = [] {
-        const char *e = getenv("BRB_TEST_FIXED_VAR_LINE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+    return brb_opt::get(brb_opt::kFixedVarLine) != 0;
 }
 
 template <class Alg>

@@ -18,6 +18,7 @@
 
 #include "byte_stream.h"
 #include "digest_line.h"
+#include "test_options.h"
 
 namespace brb_digest {
 
@@ -330,14 +331,10 @@ hipError_t launch_fixed_var_line(const uint8_t *data, uint32_t rec_len, uint64_t
     return hipGetLastError();
 }
 
-// BRB_TEST_VAR_LINE=0 keeps variable-length batches on the per-lane kernel (A/B measurements).
+// Test option "var_line" = 0 keeps variable-length batches on the per-lane kernel (A/B measurements).
 inline bool var_line_enabled()
 {
-    static const bool on = [] {
-        const char *e = getenv("BRB_TEST_VAR_LINE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+    return brb_opt::get(brb_opt::kVarLine) != 0;
 }
 
 }  // namespace brb_digest

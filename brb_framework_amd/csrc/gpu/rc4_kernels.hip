@@ -10,11 +10,11 @@
 //                      last                                (ev_kq_aio_transform.c:212-230, 281-283)
 //   rc4md5_open_kernel READ side + EvAIOReqTransform_RC4_MD5_DataValidate: one pass decrypts the
 //                      frame and feeds the decrypted payload to MD5       (:270-279, :158-184)
-#include <cstdlib>
 #include <type_traits>
 
 #include "brb_kernels.h"
 #include "rc4_device.h"
+#include "test_options.h"
 
 namespace {
 
@@ -79,7 +79,7 @@ BRB_DEV void decrypt_block(brb_io::BlockSrc &src, Snk &snk, Gen &g, uint64_t F, 
 // rounds (outputs into page-locked host memory over PCIe) 1.87 -> 1.81 ms pipelined.  With the
 // session-4 generator (S[j] read after the swap, rc4_device.h), whose steps wait on LDS as much as on
 // issue, the sink's extra VALU fit in those waits: HBM outputs 120.9 -> 118.2 us (three interleaved
-// rounds, tools/gpu_ab_env.sh BRB_TEST_RC4_SECTOR 0 1) and 187 -> 152 MB written (PMC WRITE_SIZE), so
+// rounds, the rc4_sector test option) and 187 -> 152 MB written (PMC WRITE_SIZE), so
 // every RC4 pass output now takes SectorSnk.  The open kernel, whose MD5 work already fills those
 // waits, measured slower with it (125.4 -> 134.9 us, interleaved, a build with these kernels templated on
 // the sink; not kept), so the frame and
@@ -331,11 +331,8 @@ hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, co
 {
     if (n == 0)
         return hipSuccess;
-    // BRB_TEST_RC4_SECTOR=0/1 forces the sink for A/B measurements (tools/gpu_ab_env.sh)
-    static const int force = [] {
-        const char *e = getenv("BRB_TEST_RC4_SECTOR");
-        return e ? (e[0] == '1' ? 1 : 0) : -1;
-    }();
+    // test option "rc4_sector" = 0/1 forces the sink for A/B measurements and tests
+    const int force = brb_opt::get(brb_opt::kRc4Sector);
     if (force >= 0)
         sector_out = force == 1;
     if (sector_out)

@@ -1,0 +1,22 @@
+// test_options.h -- process-wide A/B and test switches, set only through the exported test-support
+// call BRB_CryptoGPU_TestOption (batch_api.hip).  The library reads no environment variable: a
+// stray variable in a production process cannot change a code path.
+#pragma once
+
+#include <atomic>
+
+namespace brb_opt {
+
+enum Opt {
+    kRc4Sector = 0,     // -1: the launcher's choice; 0/1 force Snk / SectorSnk for the RC4 pass
+    kVarLine = 1,       // 1: variable-length digests on the line kernel; 0: per-lane kernel
+    kFixedVarLine = 2,  // 1: byte-aligned fixed-stride records on the var-line kernel; 0: record-relative
+    kVarSort = 3,       // 1: variable-length batches bucketed by block count; 0: caller order
+    kCount = 4
+};
+
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1};
+
+inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
+
+}  // namespace brb_opt

@@ -196,7 +196,7 @@ struct BRB_TransformBatcher {
     int n_rounds = 1;          // 2 when pipelined
     int cur = 0;               // the round Read/Write fill
     int dev = 0;
-    // test hook (BRB_TEST_BATCHER_FAULT=k, read at Create): the k-th kernel launch of a round is
+    // test support (BRB_TransformBatcherInjectFault): the k-th kernel launch of every round is
     // reported as failed without running, so the tests can check that a failed round is dropped
     // exactly once (the groups launched before it ran; nothing runs twice)
     int fault_launch = -1;
@@ -274,8 +274,6 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     b->zc = zc;
     b->n_rounds = pipelined ? 2 : 1;
     b->enabled.assign(max_conns, 0);
-    if (const char *f = getenv("BRB_TEST_BATCHER_FAULT"))
-        b->fault_launch = atoi(f);
     // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
     b->max_items = 4 * uint64_t(max_conns);
     b->out_cap = up(max_round_bytes + kHdr * b->max_items, kAlign);
@@ -283,7 +281,12 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     hipError_t e;
     if ((e = hipGetDevice(&b->dev)) != hipSuccess || (e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc(&b->d_states, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess ||
-        (e = hipMemset(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State))) != hipSuccess) {
+        // On the batcher's own stream and drained here.  A plain hipMemset runs on the legacy default
+        // stream, which the non-blocking `stream` does not wait for: behind other work on the default
+        // stream it could land after Enable's state copies and a round's kernels, zeroing live states
+        // (the all-zero state of tests/test_batcher.py::test_states_survive_busy_default_stream).
+        (e = hipMemsetAsync(b->d_states, 0, size_t(2) * max_conns * sizeof(BRB_RC4_State), b->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(b->stream)) != hipSuccess) {
         fail_hip("transform batcher allocation", e);
         delete b;
         return nullptr;
@@ -511,7 +514,7 @@ static int enqueue_round(BRB_TransformBatcher *b, Round &R, bool *started)
         const uint64_t *ooffs = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_ooffs);
         const uint64_t *salts = reinterpret_cast<const uint64_t *>(R.d_meta + g.o_salts);
         if (int64_t(gi) == b->fault_launch)
-            return fail_hip("kernel launch (BRB_TEST_BATCHER_FAULT)", hipErrorLaunchFailure);
+            return fail_hip("kernel launch (injected fault)", hipErrorLaunchFailure);
         if (b->zc) {
             // inputs read in place over PCIe, outputs written into the page-locked output arena
             if (b->algo == BRB_CRYPTO_FUNC_RC4) {
@@ -552,11 +555,22 @@ static int enqueue_round(BRB_TransformBatcher *b, Round &R, bool *started)
     return BRB_BATCH_OK;
 }
 
+// A dropped round: every buffer's callback fires with valid = BRB_TRANSFORM_DROPPED (no output), in
+// submission order, so an event loop learns which buffers were lost without parsing LastError.
+static void drop_round(Round &R, BRB_TransformDone done, void *user)
+{
+    if (done)
+        for (const Item &it : R.items)
+            done(user, it.conn, it.op, nullptr, 0, BRB_TRANSFORM_DROPPED);
+    R.reset();
+}
+
 // enqueue_round, and on failure drop the round: it is never retried, because the groups enqueued
 // before the failure may already have advanced their connections' RC4 states and running them again
 // would advance those states twice.  The streams are drained first, so no copy still reads an arena
-// that the next round refills.  Returns BRB_BATCH_OK or BRB_BATCH_NOT_DONE (reason in LastError).
-static int launch_round(BRB_TransformBatcher *b, Round &R)
+// that the next round refills.  Returns BRB_BATCH_OK, or BRB_BATCH_DROPPED after the dropped
+// buffers' callbacks (reason in LastError).
+static int launch_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user)
 {
     bool started = false;
     if (enqueue_round(b, R, &started) == BRB_BATCH_OK)
@@ -568,13 +582,13 @@ static int launch_round(BRB_TransformBatcher *b, Round &R)
     const std::string why = brb_api::t_err;
     set_err("%s; round of %zu buffers dropped%s", why.c_str(), R.items.size(),
             started ? " (groups launched before the failure have advanced their connections' states)" : "");
-    R.reset();
-    return BRB_BATCH_NOT_DONE;
+    drop_round(R, done, user);
+    return BRB_BATCH_DROPPED;
 }
 
 // Waits for round R and hands every result back in submission order; the k-th read item of a
 // group has valid flag k of that group.  Returns the number of buffers delivered, or -1 when the
-// round failed on the device (it is dropped without callbacks; reason in LastError).
+// round failed on the device (dropped: drop_round's callbacks; reason in LastError).
 static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user)
 {
     hipError_t e;
@@ -582,7 +596,7 @@ static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDon
         fail_hip("round completion", e);
         const std::string why = brb_api::t_err;
         set_err("%s; round of %zu buffers dropped", why.c_str(), R.items.size());
-        R.reset();
+        drop_round(R, done, user);
         return -1;
     }
     std::vector<uint32_t> next_in_group(R.group_valid.size(), 0);
@@ -625,22 +639,24 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
     if ((e = g.error()) != hipSuccess)
         return fail_hip("hipSetDevice", e);
     int64_t total = 0;
+    bool dropped = false;
     Round &prev = b->r[b->cur ^ (b->n_rounds - 1)];
     if (b->n_rounds == 2 && prev.in_flight) {   // the round FlushAsync left running comes first
         const int64_t n = deliver_round(b, prev, done, user);
         if (n < 0)
-            return BRB_BATCH_NOT_DONE;          // the current round stays pending
-        total += n;
+            dropped = true;                      // the current round still runs below
+        else
+            total += n;
     }
     Round &R = b->r[b->cur];
     if (collect(b, R) == 0) {
         R.reset();
-        return total;
+        return dropped ? BRB_BATCH_DROPPED : total;
     }
-    if (launch_round(b, R) != BRB_BATCH_OK)
-        return BRB_BATCH_NOT_DONE;
+    if (launch_round(b, R, done, user) != BRB_BATCH_OK)
+        return BRB_BATCH_DROPPED;
     const int64_t n = deliver_round(b, R, done, user);
-    return n < 0 ? BRB_BATCH_NOT_DONE : total + n;
+    return n < 0 || dropped ? BRB_BATCH_DROPPED : total + n;
 }
 
 int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
@@ -657,19 +673,30 @@ int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDon
     if ((e = g.error()) != hipSuccess)
         return fail_hip("hipSetDevice", e);
     Round &R = b->r[b->cur], &prev = b->r[b->cur ^ 1];
-    if (collect(b, R) == 0) {
+    // enqueue this round first so the GPU has it while the previous round's callbacks run; a failed
+    // one is dropped (its callbacks fire), and the previous round is still delivered below
+    bool dropped = false;
+    if (collect(b, R) == 0)
         R.reset();
-    } else if (launch_round(b, R) != BRB_BATCH_OK) {
-        // enqueue this round first so the GPU has it while the previous round's callbacks run; a
-        // failed one is dropped, and the previous round (if running) is delivered by the next flush
-        return BRB_BATCH_NOT_DONE;
-    }
+    else if (launch_round(b, R, done, user) != BRB_BATCH_OK)
+        dropped = true;
     if (R.in_flight)
         b->cur ^= 1;   // Read/Write now fill the other arena (the previous round's, once delivered)
-    if (!prev.in_flight)
-        return 0;
-    const int64_t n = deliver_round(b, prev, done, user);
-    return n < 0 ? BRB_BATCH_NOT_DONE : n;
+    int64_t n = 0;
+    if (prev.in_flight)
+        n = deliver_round(b, prev, done, user);
+    return n < 0 || dropped ? BRB_BATCH_DROPPED : n;
+}
+
+int BRB_TransformBatcherInjectFault(BRB_TransformBatcher *b, int launch)
+{
+    brb_api::clear_err();
+    if (!b) {
+        set_err("NULL batcher");
+        return BRB_BATCH_BADARG;
+    }
+    b->fault_launch = launch;
+    return BRB_BATCH_OK;
 }
 
 }  // extern "C"

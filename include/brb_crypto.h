@@ -109,6 +109,7 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
 #define BRB_BATCH_OK        1
 #define BRB_BATCH_NOT_DONE  0
 #define BRB_BATCH_BADARG   (-1)
+#define BRB_BATCH_DROPPED  (-2)   /* transform batcher: a round was dropped (see Flush)         */
 
 /* flags */
 #define BRB_BATCH_HOST      0x0u   /* pointers are host memory: copied in and out by the call      */
@@ -257,6 +258,8 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
 #define BRB_BATCHER_PIPELINED     0x200
 typedef struct BRB_TransformBatcher BRB_TransformBatcher;
 typedef void (*BRB_TransformDone)(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid);
+/* `valid` of a buffer whose round was dropped (out = NULL, out_len = 0): see Flush. */
+#define BRB_TRANSFORM_DROPPED (-1)
 /* NULL on failure (reason in BRB_CryptoGPU_LastError).  A round holds at most max_round_bytes of
  * input and 4 * max_conns buffers; Read/Write return 0 when it is full (Flush, then submit again). */
 BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t max_round_bytes, int algo);
@@ -269,10 +272,14 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
  * chunks, so a round shared by T threads may report full up to T chunks (64 buffers, 128 KiB) early. */
 int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
 int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
-/* Runs the round; returns the number of buffers delivered, -1 for bad arguments, or 0 with LastError
- * set on a device error.  A round that fails on the device is dropped without callbacks and never
- * re-run (kernels launched before the failure may have advanced their connections' states; running
- * them again would advance them twice).  On a pipelined batcher Flush first delivers the round
+/* Runs the round; returns the number of buffers delivered, or -1 for bad arguments.  A round that
+ * fails on the device is dropped and never re-run (kernels launched before the failure may have
+ * advanced their connections' states; running them again would advance them twice): each of its
+ * buffers still gets its callback, in order, with valid = BRB_TRANSFORM_DROPPED, out = NULL and
+ * out_len = 0, and the call returns BRB_BATCH_DROPPED (-2) with the reason in LastError -- also when
+ * another round was delivered in the same call, whose buffers came back through their callbacks as
+ * usual.  Such connections are out of step with their peers, as after a lost buffer in the
+ * reference, and are re-keyed with Enable.  On a pipelined batcher Flush first delivers the round
  * FlushAsync left running, so Flush drains everything.  A batcher's calls run on the device it was
  * created on and leave the calling thread's current device unchanged. */
 int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
@@ -284,6 +291,11 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
 int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
 /* Copies a connection's current state (op = READ or WRITE) back to the host (tests, migration). */
 int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op, BRB_RC4_State *out);
+/* Test support, not for production use: from now on the `launch`-th kernel launch (0-based) of every
+ * round reports a failure without running, so a test can watch a round being dropped; -1 turns it
+ * off.  Returns 1, or -1 for a NULL batcher.  (Replaces round 2's BRB_TEST_BATCHER_FAULT variable:
+ * the library reads no environment variable.) */
+int BRB_TransformBatcherInjectFault(BRB_TransformBatcher *b, int launch);
 
 /* ---- base64 -----------------------------------------------------------------------
  * Encode = brb_base64_encode_to_mb (base64.c:304-361) for n records: record i = data[offsets[i] ..
@@ -343,6 +355,14 @@ const char *BRB_CryptoGPU_LastError(void);
  * same `p`. */
 int BRB_CryptoGPU_HostRegister(void *p, uint64_t len);
 int BRB_CryptoGPU_HostUnregister(void *p);
+/* Test support, not for production use: process-wide A/B switches of the kernel selection, the only
+ * way to change them (the library reads no environment variable).  "rc4_sector" -1/0/1 (launcher's
+ * choice / force the per-stream sink / force the whole-sector sink of the RC4 pass), "var_line" 1/0
+ * (variable-length digests on the line kernel / on the per-lane kernel), "fixed_var_line" 1/0
+ * (unaligned fixed-stride records on the line kernel / record-relative kernel), "var_sort" 1/0
+ * (variable-length batches bucketed by block count / in caller order).  Returns 1 and the previous
+ * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
+int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */
 const char *BRB_CryptoGPU_Version(void);
 

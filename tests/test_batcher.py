@@ -33,6 +33,37 @@ def _check_round(got, expect, rnd):
 def test_event_loop_rounds(brb, orc, torch_dev, algo, zero_copy, pipelined):
     """pipelined: BRB_BATCHER_PIPELINED, each round started with FlushAsync, whose results come
     back from the next round's FlushAsync (the last from Flush)."""
+    _event_loop(brb, orc, algo, zero_copy, pipelined)
+
+
+def test_event_loop_after_rc4_and_base64(brb, orc, torch_dev):
+    """Regression, in the order that failed in round 2: a full-size RC4 pass and a
+    base64 round trip enqueued on the default stream, then -- without waiting for them -- the
+    pipelined copy-mode RC4 event loop.  The batcher's Create used to clear the state table on the
+    default stream behind that work, after Enable had uploaded the states (GetState read zeros)."""
+    torch = torch_dev
+    n, L = 65536, 1500
+    data = torch.from_numpy(workload.gen_records(0x5EED0002, 0, n, L)).cuda()
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * L
+    lens = torch.full((n,), L, dtype=torch.int32, device="cuda")
+    keys = [bytes([k & 255, k >> 8]) * 8 for k in range(n)]
+    st = torch.from_numpy(brb.rc4_states(keys)).cuda()
+    Lb = brb.lib()
+    s = torch.cuda.current_stream().cuda_stream
+    flags = brb.BATCH_DEVICE | brb.BATCH_ASYNC
+    for _ in range(4):
+        assert Lb.BRB_RC4_CryptBatch(st.data_ptr(), data.data_ptr(), data.data_ptr(), offs.data_ptr(),
+                                     lens.data_ptr(), n, flags, s) == 1
+    T = 4 * ((L + 2) // 3)
+    toffs = torch.arange(n, dtype=torch.int64, device="cuda") * T
+    text = torch.zeros(n * T, dtype=torch.uint8, device="cuda")
+    assert Lb.BRB_Base64EncodeBatch(data.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, text.data_ptr(),
+                                    toffs.data_ptr(), flags, s) == 1
+    _event_loop(brb, orc, 1, False, True)
+    torch.cuda.synchronize()
+
+
+def _event_loop(brb, orc, algo, zero_copy, pipelined):
     rng = np.random.default_rng(algo)
     C = 300
     keys = [rng.integers(0, 256, int(rng.integers(4, 32)), dtype=np.uint8).tobytes() for _ in range(C)]
@@ -221,22 +252,24 @@ def test_pipelined_edges(brb, orc, torch_dev):
     b.close()                                    # waits for the running round
 
 
-def test_failed_round_is_dropped_once(brb, orc, torch_dev, monkeypatch):
+def test_failed_round_is_dropped_once(brb, orc, torch_dev):
     """A round whose enqueue fails part-way is dropped, never re-run (transform_batcher.hip
-    launch_round).  BRB_TEST_BATCHER_FAULT=1 makes the second kernel launch of a round report a
-    failure without running: connection 0 has two read buffers (sub-rounds 0 and 1), so group 0
-    (its first buffer) runs and group 1 does not.  Flush returns 0 with the reason; the next Flush has
-    nothing to run; the state shows the first buffer applied exactly once."""
-    monkeypatch.setenv("BRB_TEST_BATCHER_FAULT", "1")
+    launch_round).  BRB_TransformBatcherInjectFault(b, 1) makes the second kernel launch of a round
+    report a failure without running: connection 0 has two read buffers (sub-rounds 0 and 1), so
+    group 0 (its first buffer) runs and group 1 does not.  Flush returns BRB_BATCH_DROPPED with the
+    reason, and both buffers' callbacks fire with valid = BRB_TRANSFORM_DROPPED and no output; the
+    next Flush has nothing to run; the state shows the first buffer applied exactly once."""
     b = brb.TransformBatcher(4, 1 << 20, 1)
-    monkeypatch.delenv("BRB_TEST_BATCHER_FAULT")
+    b.inject_fault(1)
     key = b"faultkey"
     b.enable(0, key)
     st = orc.rc4_init(key)
     first = bytes(range(200))
     assert b.read(0, first) == 1 and b.read(0, bytes(100)) == 1
-    with pytest.raises(RuntimeError, match="dropped"):
+    with pytest.raises(RuntimeError, match="dropped") as ei:
         b.flush()
+    assert ei.value.results == [(0, 0, b"", brb.TRANSFORM_DROPPED)] * 2
+    b.inject_fault(-1)
     assert b.flush() == []                         # the failed round is gone, nothing re-runs
     st_once, _ = orc.rc4_crypt(st, first)
     assert b.state(0, 0) == st_once                # group 0 ran once; group 1 never ran
@@ -245,4 +278,45 @@ def test_failed_round_is_dropped_once(brb, orc, torch_dev, monkeypatch):
     got = b.flush()
     st_twice, want = orc.rc4_crypt(st_once, first)
     assert got == [(0, 0, want, 1)] and b.state(0, 0) == st_twice
+    b.close()
+
+
+def test_pipelined_drop_keeps_delivered_round(brb, orc, torch_dev):
+    """Pipelined Flush delivers the round FlushAsync left running, then the current round fails:
+    the delivered round's results still come back through their callbacks, the dropped buffers'
+    callbacks carry BRB_TRANSFORM_DROPPED, and the call returns BRB_BATCH_DROPPED (not 0)."""
+    key = b"pipe-drop"
+    b = brb.TransformBatcher(2, 1 << 16, 1, pipelined=True)
+    b.enable(0, key)
+    st = orc.rc4_init(key)
+    assert b.read(0, b"first round") == 1
+    assert b.flush_async() == []                   # round 1 runs
+    b.inject_fault(0)                              # every launch of the next round fails
+    assert b.read(0, b"second round") == 1
+    with pytest.raises(RuntimeError, match="dropped") as ei:
+        b.flush()
+    st, want = orc.rc4_crypt(st, b"first round")
+    assert ei.value.results == [(0, 0, want, 1), (0, 0, b"", brb.TRANSFORM_DROPPED)]
+    assert b.state(0, 0) == st
+    b.close()
+
+
+def test_states_survive_busy_default_stream(brb, orc, torch_dev):
+    """Regression (round-3 cause of the all-zero RC4 state): Create zeroed the state
+    table with hipMemset, i.e. on the legacy default stream, which the batcher's non-blocking stream
+    does not wait for.  With the default stream busy (a long kernel queued on it first), that memset
+    ran after Enable's state uploads and after the first round, and GetState read zeros.  The table
+    is now cleared on the batcher's own stream before Create returns."""
+    torch = torch_dev
+    key = b"busy-default-stream"
+    torch.cuda._sleep(200_000_000)                # ~0.1 s of spinning on the default stream
+    b = brb.TransformBatcher(4, 1 << 16, 1, pipelined=True)
+    b.enable(0, key)
+    st = orc.rc4_init(key)
+    assert b.read(0, b"hello, busy stream") == 1
+    assert b.flush_async() == []
+    st, want = orc.rc4_crypt(st, b"hello, busy stream")
+    assert b.flush() == [(0, 0, want, 1)]
+    torch.cuda.synchronize()                       # the default stream's work has all landed
+    assert b.state(0, 0) == st and b.state(0, 1) == orc.rc4_init(key)
     b.close()

@@ -388,45 +388,32 @@ def test_rc4md5_full_shape(brb, orc, torch_dev):
     assert np.array_equal(got[:, 30:], payload.reshape(n, L))
 
 
-_SECTOR_SCRIPT = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-import brb_framework_amd as brb, oracle
-from brb_framework_amd import workload
-rng = np.random.default_rng(11)
-for base in (0, 1, 2, 3):
-    lens = rng.integers(0, 3000, 257).astype(np.uint32)
-    gaps = rng.integers(0, 6, 257)
-    offs = (base + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64) + gaps[:-1])])).astype(np.uint64)
-    total = int(offs[-1] + lens[-1]) + 8
-    data = workload.gen_records(0x5EED00A1, base, 1, total)
-    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(len(offs))]
-    states = brb.rc4_states(keys)
-    want = data.copy()
-    for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
-        s2, ob = oracle.rc4_crypt(states[i].tobytes(), data[o:o + n].tobytes())
-        want[o:o + n] = np.frombuffer(ob, np.uint8)
-    t = torch.from_numpy(data).cuda()
-    brb.rc4_crypt_batch(torch.from_numpy(states).cuda(), t, torch.from_numpy(offs).cuda(), torch.from_numpy(lens).cuda())
-    assert np.array_equal(t.cpu().numpy(), want), base
-print("sector sink ok")
-"""
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("sector", ["1", "0"])
-def test_rc4_sector_sink_ragged(brb, sector):
+@pytest.mark.parametrize("sector", [1, 0])
+def test_rc4_sector_sink_ragged(brb, orc, sector):
     """Both output sinks of the RC4 pass on ragged, packed streams at every byte offset, device mode
     in place, against the oracle: brb_io::SectorSnk (whole aligned sectors, the default for every
-    output) and the per-stream Snk it replaced (kept for A/B runs).  The sink is forced with
-    BRB_TEST_RC4_SECTOR, which the library reads once per process: one child process each."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _SECTOR_SCRIPT, root], env=dict(os.environ, BRB_TEST_RC4_SECTOR=sector),
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "sector sink ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    output) and the per-stream Snk it replaced (kept for A/B runs), forced with the "rc4_sector"
+    test option (BRB_CryptoGPU_TestOption)."""
+    import torch
+    rng = np.random.default_rng(11)
+    with brb.TestOption("rc4_sector", sector):
+        for base in (0, 1, 2, 3):
+            lens = rng.integers(0, 3000, 257).astype(np.uint32)
+            gaps = rng.integers(0, 6, 257)
+            offs = (base + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64) + gaps[:-1])])).astype(np.uint64)
+            total = int(offs[-1] + lens[-1]) + 8
+            data = workload.gen_records(0x5EED00A1, base, 1, total)
+            keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(len(offs))]
+            states = brb.rc4_states(keys)
+            want = data.copy()
+            for i, (o, n) in enumerate(zip(offs.tolist(), lens.tolist())):
+                s2, ob = orc.rc4_crypt(states[i].tobytes(), data[o:o + n].tobytes())
+                want[o:o + n] = np.frombuffer(ob, np.uint8)
+            t = torch.from_numpy(data).cuda()
+            brb.rc4_crypt_batch(torch.from_numpy(states).cuda(), t, torch.from_numpy(offs).cuda(),
+                                torch.from_numpy(lens).cuda())
+            assert np.array_equal(t.cpu().numpy(), want), base
 
 
 @pytest.mark.gpu
