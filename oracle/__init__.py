@@ -35,7 +35,8 @@ def lib() -> ctypes.CDLL:
             "orc_md5": (None, [vp, u64, vp]),
             "orc_sha1_init": (None, [vp]), "orc_sha1_update": (None, [vp, vp, ctypes.c_size_t]),
             "orc_sha1_final": (None, [vp, vp]), "orc_sha1": (None, [vp, u64, vp]),
-            "orc_bf_pi_words": (None, [vp]), "orc_bf_init": (None, [vp, vp, ctypes.c_int]),
+            "orc_bf_pi_words": (None, [vp]), "orc_md5_consts": (None, [vp, vp, vp, vp]),
+            "orc_sha1_consts": (None, [vp, vp]), "orc_bf_init": (None, [vp, vp, ctypes.c_int]),
             "orc_bf_encrypt": (None, [vp, vp, vp]), "orc_bf_decrypt": (None, [vp, vp, vp]),
             "orc_bf_ecb": (None, [vp, vp, u64, ctypes.c_int, ctypes.c_int]),
             "orc_membuf_key": (None, [ctypes.c_uint, vp]),
@@ -131,6 +132,20 @@ def bf_pi_words() -> list:
     w = (ctypes.c_uint32 * 1042)()
     lib().orc_bf_pi_words(w)
     return list(w)
+
+
+def md5_consts() -> dict:
+    """The MD5 constants the restatement uses: T, message word and rotation per step, IV."""
+    a = [np.zeros(64, np.uint32) for _ in range(3)] + [np.zeros(4, np.uint32)]
+    lib().orc_md5_consts(*[_p(x) for x in a])
+    return dict(zip(("T", "word", "rot", "iv"), [x.tolist() for x in a]))
+
+
+def sha1_consts() -> dict:
+    """The SHA-1 constants the restatement uses: round constant per step, IV."""
+    k, iv = np.zeros(80, np.uint32), np.zeros(5, np.uint32)
+    lib().orc_sha1_consts(_p(k), _p(iv))
+    return {"k80": k.tolist(), "iv": iv.tolist()}
 
 
 def bf_init(key: bytes, key_len: int | None = None) -> BfCtx:

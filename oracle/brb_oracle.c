@@ -28,6 +28,17 @@ static void md5_tables(void)
         md5_T[i] = (uint32_t)(uint64_t)floor(fabs(sin((double)(i + 1))) * 4294967296.0);
 }
 
+/* Message word of step i: RFC 1321 §3.4's per-round index progressions. */
+static int md5_word(int i)
+{
+    switch (i >> 4) {
+    case 0: return i;
+    case 1: return (5 * i + 1) & 15;
+    case 2: return (3 * i + 5) & 15;
+    default: return (7 * i) & 15;
+    }
+}
+
 /* One compression of c->in into c->buf (md5.c:170-253). */
 static void orc_md5_transform(orc_md5_ctx *c)
 {
@@ -35,14 +46,13 @@ static void orc_md5_transform(orc_md5_ctx *c)
     for (int i = 0; i < 64; i++) {
         int r = i >> 4;
         uint32_t f;
-        int g;
         switch (r) {       /* F1..F4 of libbrb_data.h:845-848 */
-        case 0: f = d ^ (b & (cc ^ d)); g = i; break;
-        case 1: f = cc ^ (d & (b ^ cc)); g = (5 * i + 1) & 15; break;
-        case 2: f = b ^ cc ^ d; g = (3 * i + 5) & 15; break;
-        default: f = cc ^ (b | ~d); g = (7 * i) & 15; break;
+        case 0: f = d ^ (b & (cc ^ d)); break;
+        case 1: f = cc ^ (d & (b ^ cc)); break;
+        case 2: f = b ^ cc ^ d; break;
+        default: f = cc ^ (b | ~d); break;
         }
-        uint32_t t = a + f + c->in[g] + md5_T[i];     /* MD5STEP, libbrb_data.h:851 */
+        uint32_t t = a + f + c->in[md5_word(i)] + md5_T[i];     /* MD5STEP, libbrb_data.h:851 */
         a = d;
         d = cc;
         cc = b;
@@ -137,6 +147,9 @@ void orc_md5(const void *p, uint64_t len, uint8_t out[16])
 /* SHA-1 -- libbrb_core/crypto/sha1.c                                                           */
 /* =========================================================================================== */
 
+/* FIPS 180-1 round constants, one per 20 steps (the reference's R0/R1..R4 macros, sha1.c:54-58). */
+static const uint32_t sha1_K[4] = {0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u};
+
 /* Compression of one 64-byte block (sha1.c:75-130).  With SHA1HANDSOFF undefined the reference
  * expands the schedule inside the caller's block: on return the block holds W[64..79] in host
  * (little-endian) order.  `block` is mutated the same way here. */
@@ -150,11 +163,12 @@ static void orc_sha1_transform_x(uint32_t st[5], uint8_t *block, int mutate)
         W[i] = rotl32(W[i - 3] ^ W[i - 8] ^ W[i - 14] ^ W[i - 16], 1);
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
     for (int i = 0; i < 80; i++) {
-        uint32_t f, k;
-        if (i < 20) { f = (b & c) | (~b & d); k = 0x5A827999u; }
-        else if (i < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1u; }
-        else if (i < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDCu; }
-        else { f = b ^ c ^ d; k = 0xCA62C1D6u; }
+        uint32_t f;
+        const uint32_t k = sha1_K[i / 20];
+        if (i < 20) f = (b & c) | (~b & d);
+        else if (i < 40) f = b ^ c ^ d;
+        else if (i < 60) f = (b & c) | (b & d) | (c & d);
+        else f = b ^ c ^ d;
         uint32_t t = rotl32(a, 5) + f + e + k + W[i];
         e = d;
         d = c;
@@ -855,4 +869,28 @@ void orc_gen_records(uint64_t seed, uint64_t r0, uint64_t n, uint32_t L, uint8_t
                 o[k + b] = (uint8_t)(v >> (8 * b));
         }
     }
+}
+
+/* The constants the restatement uses, for tests/test_ref_tables.py (pinned to the reference's
+ * source text through tests/golden/ref_tables.json): MD5 T, message word and rotation per step and
+ * the IV; SHA-1 round constant per step and the IV. */
+void orc_md5_consts(uint32_t T[64], uint32_t word[64], uint32_t rot[64], uint32_t iv[4])
+{
+    orc_md5_ctx c;
+    orc_md5_init(&c);
+    for (int i = 0; i < 64; i++) {
+        T[i] = md5_T[i];
+        word[i] = (uint32_t)md5_word(i);
+        rot[i] = md5_shift[i >> 4][i & 3];
+    }
+    memcpy(iv, c.buf, 16);
+}
+
+void orc_sha1_consts(uint32_t k80[80], uint32_t iv[5])
+{
+    orc_sha1_ctx c;
+    orc_sha1_init(&c);
+    for (int i = 0; i < 80; i++)
+        k80[i] = sha1_K[i / 20];
+    memcpy(iv, c.state, 20);
 }

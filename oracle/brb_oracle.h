@@ -68,6 +68,8 @@ typedef struct {                 /* same layout as BRB_BLOWFISH_CTX, libbrb_data
 
 /* pi-derived tables by BBP digit extraction (independent of tools/gen_pi_tables.py) */
 void orc_bf_pi_words(uint32_t out[1042]);
+void orc_md5_consts(uint32_t T[64], uint32_t word[64], uint32_t rot[64], uint32_t iv[4]);
+void orc_sha1_consts(uint32_t k80[80], uint32_t iv[5]);
 void orc_bf_init(orc_bf_ctx *c, const unsigned char *key, int key_len);
 void orc_bf_encrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr);
 void orc_bf_decrypt(const orc_bf_ctx *c, uint64_t *xl, uint64_t *xr);
