@@ -37,7 +37,10 @@ METRIC = "GiB/s (device-resident) + Mrecords/s over 1500B buffers at 1/2/4/8 MI3
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 L3_BYTES = 256 << 20
 SIMDS = 1024                   # 256 CUs x 4 SIMDs
-CLOCK_GHZ = 2.4                # max shader clock (MI355X_MICROARCH.md "Chip-level parameters")
+CLOCK_GHZ = 2.1                # shader clock the chip holds with every CU issuing these kernels:
+                               # 2.10-2.16 GHz measured in-kernel (s_memtime / s_memrealtime,
+                               # profiles/r02d_md5_tput.txt); 2.4 GHz is the maximum, held only with
+                               # a few CUs busy (MI355X_MICROARCH.md "DVFS give-back")
 VALU_PEAK_CYC = 2.0            # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (guide, "SIMD")
 LONE_WAVE_CYC = {"md5": 4.85, "sha1": 4.54}   # one wave per SIMD: measured issue cost per VALU
                                               # instruction (tools/mb/valu_latency.hip)
@@ -66,6 +69,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
+    ap.add_argument("--test-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="BRB_CryptoGPU_TestOption before the run (A/B of kernel selections)")
+    ap.add_argument("--mark-timed-region", action="store_true",
+                    help="enqueue a tiny spin kernel (at::cuda spin_kernel) right before and right after each "
+                         "timed region, outside the timing, so a rocprofv3 kernel trace can select exactly the "
+                         "timed dispatches (tools/collect_profiles.py)")
     return ap.parse_args()
 
 
@@ -178,6 +187,11 @@ def main():
             dist.init_process_group("gloo")
     if not brb.gpu_available():
         raise SystemExit("libbrb_crypto_gpu: " + brb.lib().BRB_CryptoGPU_LastError().decode())
+    for opt in args.test_option:
+        name, value = opt.split("=")
+        brb.test_option(name, int(value))
+    global MARK
+    MARK = args.mark_timed_region
 
     def barrier():
         if dist is not None:
@@ -256,6 +270,9 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
     return n, int(max_over_ranks(float(k)))
 
 
+MARK = False     # --mark-timed-region
+
+
 def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     """K steps between barrier + synchronize on both sides; step k is enqueued on
     streams[k % len(streams)] straight through the C ABI (pre-resolved ctypes arguments, so the
@@ -263,6 +280,9 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     region (one pair, nothing between kernels).  Returns (wall seconds max over ranks,
     event-timed seconds on stream 0)."""
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if MARK:             # sentinel before the region, drained before t0
+        with torch.cuda.stream(streams[0]):
+            torch.cuda._sleep(1)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -273,6 +293,10 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     e1.record(streams[0])
     torch.cuda.synchronize()
     barrier()
+    if MARK:             # sentinel after the region, enqueued after the timing ended
+        with torch.cuda.stream(streams[0]):
+            torch.cuda._sleep(1)
+        torch.cuda.synchronize()
     wall = max_over_ranks(time.perf_counter() - t0)
     return wall, e0.elapsed_time(e1) / 1e3
 
@@ -330,6 +354,14 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     for j, s_ in enumerate(all_streams):                        # one eager call per stream
         launch(j, s_, j)
     main_streams = [stream] if n_streams == 1 else side[:n_streams]
+    cfg5 = None
+    if cfg_id == 2 and args.op == "md5" and not args.no_cfg5 and not args.records_per_gpu and not args.rec_len:
+        # the cfg5 sub-measurement (>= 1.3 s of GPU work) runs BEFORE the headline's W warm-up steps:
+        # a fresh MI355X starts at a low clock and takes hundreds of ms to reach its loaded state, which
+        # a short W (the driver passes --warmup 5 = 0.1 ms) does not cover (r02: 22.46 us per launch
+        # after 5 warm-up steps, 20.99 us in steady state).  The order changes no work and no timing
+        # rule: each region is still W untimed + K timed steps between barrier + synchronize.
+        cfg5 = bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log)
     # warm up on the streams the timed region uses (so rocprof's per-kernel average over the whole
     # run describes the same back-to-back launches as the timed region)
     n_warm, n_steps = warm_up(args, launch_raw, main_streams, torch, max_over_ranks)
@@ -369,7 +401,9 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "dtype": "u32",
         "data": "synthetic (SURVEY §8(d) splitmix64 generator, HBM-resident, L3-defeating rotation of "
                 f"{n_rot} copies)",
-        "config": {"workload": (cfg["name"] if not args.rec_len else f"{n_rank} x {L} B records (cfg{cfg_id} shape, --rec-len)")
+        "config": {"workload": ((cfg["name"] if args.op == "md5" else cfg["name"].replace(" MD5", " SHA-1") + " (SHA-1 on the "
+                                 f"cfg{cfg_id} shape; BASELINE's digest is MD5)")
+                                if not args.rec_len else f"{n_rank} x {L} B records (cfg{cfg_id} shape, --rec-len)")
                    + (f" (shard of {n_rank} records/GPU)" if cfg_id == 5 else "")
                    + (f"; the same batch on each of {world} GPUs" if world > 1 and cfg_id != 5 else ""),
                    "op": f"{'BRB_MD5BatchFixed' if args.op == 'md5' else 'BrbSha1_BatchFixed'} (device mode)",
@@ -393,8 +427,10 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         result["pcie_inclusive"] = bench_pcie_digest(fn, host, L, n_rank, width, log)
     del bufs, outs
     torch.cuda.empty_cache()
-    if cfg_id == 2 and args.op == "md5" and not args.no_cfg5 and not args.records_per_gpu and not args.rec_len:
-        result["cfg5"] = bench_cfg5(args, rank, world, dev, stream, barrier, max_over_ranks, log)
+    if cfg5 is not None:
+        result["cfg5"] = cfg5
+        result["order"] = ("cfg5 sub-measurement first (GPU at its loaded clock), then the headline's W warm-up + K "
+                           "timed steps, then the host-inclusive and CPU legs")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_digest(args, host, L, n_rank, log)
     log(f"[bench] launch avg {avg_kern_s * 1e6:.1f} us -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.1%} of HBM peak)")
@@ -794,6 +830,26 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                      "note": "algorithmic bytes read+written per step; the bound in practice is the per-byte "
                              "RC4 dependency chain through LDS (DESIGN.md)"},
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op == "rc4":
+        th = cpu_threads()
+        m = min(n, 16384)
+        hst = st0[:m].copy()
+        hd = host[: m * L].copy()
+        ho = np.arange(m, dtype=np.uint64) * L
+        hl = np.full(m, L, np.uint32)
+        res = {}
+        for t_ in (th, 1):
+            mm = m if t_ > 1 else m // 16
+            reps, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < args.cpu_seconds / 2:
+                oracle.rc4_crypt_batch(hst, hd, ho[:mm], hl[:mm], threads=t_)
+                reps += 1
+            res[t_] = (mm * L * reps / (time.perf_counter() - t0) / 2**30, reps, mm)
+        gib, reps, mm = res[th]
+        result["cpu_baseline"] = {"value": round(gib, 3), "unit": "GiB/s", "kind": "port", **core_counts(th, res[1][0]),
+                                  "single_core_gib_s": round(res[1][0], 4),
+                                  "sample": f"oracle BRB_RC4_Crypt restatement in place on {mm} connections x {L} B, "
+                                            f"{reps} passes, {th} pthreads"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.op == "rc4md5":
         th = cpu_threads()
         m = min(n, 16384)
@@ -883,6 +939,28 @@ def bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                      **traffic_fields(args.pmc_summary, f"var_{args.op}"),
                      "launch_us_avg": round(step_s * 1e6, 2), "bytes_per_launch": payload},
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle     # test infrastructure: the CPU restatement is the baseline, never the product
+        th = cpu_threads()
+        fn = oracle.md5_batch if args.op == "md5var" else oracle.sha1_batch
+        res = {}
+        for t_ in (th, 1):
+            m = n if t_ > 1 else n // 16
+            fn(host, offs_h[:256], lens_h[:256], threads=t_)
+            reps, t0 = 0, time.perf_counter()
+            while True:
+                dg = fn(host, offs_h[:m], lens_h[:m], threads=t_)
+                reps += 1
+                if time.perf_counter() - t0 >= args.cpu_seconds / 2:
+                    break
+            res[t_] = (int(lens_h[:m].sum()) * reps / (time.perf_counter() - t0) / 2**30, reps, m)
+        assert np.array_equal(dg[:64], got[:64])
+        gib, reps, m = res[th]
+        result["cpu_baseline"] = {"value": round(gib, 3), "unit": "GiB/s", "kind": "port", **core_counts(th, res[1][0]),
+                                  "single_core_gib_s": round(res[1][0], 4),
+                                  "sample": f"oracle/brb_oracle.c {name} restatement over the same {m} records "
+                                            f"(U[1000, 2000] B at their offsets), {reps} passes, {th} pthreads"}
+        log(f"[bench] cpu baseline {gib:.2f} GiB/s on {th} threads")
     log(f"[bench] {name}: {step_s * 1e6:.1f} us per launch")
     return result
 

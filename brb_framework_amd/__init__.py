@@ -35,6 +35,7 @@ from .crypto import (  # noqa: F401
     HostRegion,
     BATCHER_ZERO_COPY,
     BATCHER_PIPELINED,
+    BATCHER_ALL_DEVICES,
     base64_decode_batch,
     base64_encode_batch,
     blowfish_ctx_bytes,
@@ -73,5 +74,5 @@ __all__ = [
     "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "metadata_unpack_batch", "METADATA_INFO_DTYPE", "base64_decode_batch",
     "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
     "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED", "BATCH_ALL_DEVICES", "device_count",
-    "BATCH_DROPPED", "TRANSFORM_DROPPED", "TestOption", "test_option",
+    "BATCH_DROPPED", "TRANSFORM_DROPPED", "BATCHER_ALL_DEVICES", "TestOption", "test_option",
 ]

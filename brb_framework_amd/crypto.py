@@ -288,13 +288,14 @@ def md5_batch(data, offsets, lengths, out=None, stream=None, async_=False, all_d
     return _digest_var(lib().BRB_MD5Batch, 16, data, offsets, lengths, out, stream, async_, all_devices)
 
 
-def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, stream=None, async_=False):
+def md5_batch_segments(data, seg_offsets, seg_lengths, rec_first_seg, out=None, stream=None, async_=False,
+                       all_devices=False):
     """BRB_MD5BatchSegments: record i = concatenation of segments rec_first_seg[i] .. rec_first_seg[i+1]-1
     (the MetaData pack digest).  rec_first_seg has n + 1 entries."""
     n = len(rec_first_seg) - 1
     if out is None:
         out = _out_like(data, n, 16)
-    flags, h = _mode(data, stream, async_)
+    flags, h = _mode(data, stream, async_, all_devices)
     _check(lib().BRB_MD5BatchSegments(_ptr(data), _ptr(seg_offsets), _ptr(seg_lengths), _ptr(rec_first_seg), n,
                                       _ptr(out), flags, h), "BRB_MD5BatchSegments")
     return out
@@ -398,35 +399,37 @@ def _same_kind(ref, *xs):
             raise ValueError("all buffers of one batch call must be numpy (host) or all CUDA tensors (device)")
 
 
-def rc4_crypt_batch(states, data, offsets, lengths, out=None, stream=None, async_=False):
+def rc4_crypt_batch(states, data, offsets, lengths, out=None, stream=None, async_=False, all_devices=False):
     """BRB_RC4_CryptBatch: stream i = data[offsets[i]:+lengths[i]] -> out (in place when out is None).
     states: (n, 264) uint8, updated in place."""
     out = data if out is None else out
     _same_kind(data, states, out, offsets, lengths)
-    flags, h = _mode(data, stream, async_)
+    flags, h = _mode(data, stream, async_, all_devices)
     _check(lib().BRB_RC4_CryptBatch(_ptr(states), _ptr(data), _ptr(out), _ptr(offsets), _ptr(lengths), len(offsets),
                                     flags, h), "BRB_RC4_CryptBatch")
     return out
 
 
-def rc4md5_frame_batch(states, payload, offsets, lengths, salts, frames, frame_offsets, stream=None, async_=False):
+def rc4md5_frame_batch(states, payload, offsets, lengths, salts, frames, frame_offsets, stream=None, async_=False,
+                       all_devices=False):
     """BRB_RC4MD5_FrameBatch: frames[frame_offsets[i]:+30+lengths[i]] = RC4(salt|"HASH:"|MD5|NUL|payload)."""
     _same_kind(payload, states, offsets, lengths, salts, frames, frame_offsets)
-    flags, h = _mode(payload, stream, async_)
+    flags, h = _mode(payload, stream, async_, all_devices)
     _check(lib().BRB_RC4MD5_FrameBatch(_ptr(states), _ptr(payload), _ptr(offsets), _ptr(lengths), _ptr(salts),
                                        _ptr(frames), _ptr(frame_offsets), len(offsets), flags, h),
            "BRB_RC4MD5_FrameBatch")
     return frames
 
 
-def rc4md5_open_batch(states, frames, offsets, lengths, out=None, valid=None, stream=None, async_=False):
+def rc4md5_open_batch(states, frames, offsets, lengths, out=None, valid=None, stream=None, async_=False,
+                      all_devices=False):
     """BRB_RC4MD5_OpenBatch: decrypt frames (in place when out is None); returns (out, valid uint8[n])."""
     out = frames if out is None else out
     n = len(offsets)
     if valid is None:
         valid = _out_like(frames, n, 1).reshape(n)
     _same_kind(frames, states, out, offsets, lengths, valid)
-    flags, h = _mode(frames, stream, async_)
+    flags, h = _mode(frames, stream, async_, all_devices)
     _check(lib().BRB_RC4MD5_OpenBatch(_ptr(states), _ptr(frames), _ptr(out), _ptr(offsets), _ptr(lengths), n,
                                       _ptr(valid), flags, h), "BRB_RC4MD5_OpenBatch")
     return out, valid
@@ -466,16 +469,17 @@ def membuf_decrypt(buf, size, seed, offset=0, stream=None):
 
 
 # ---- base64 -------------------------------------------------------------------------
-def base64_encode_batch(data, offsets, lengths, out, out_offsets, stream=None, async_=False):
+def base64_encode_batch(data, offsets, lengths, out, out_offsets, stream=None, async_=False, all_devices=False):
     """BRB_Base64EncodeBatch: out[out_offsets[i]:+4*ceil(len/3)] = base64 of record i."""
     _same_kind(data, offsets, lengths, out, out_offsets)
-    flags, h = _mode(data, stream, async_)
+    flags, h = _mode(data, stream, async_, all_devices)
     _check(lib().BRB_Base64EncodeBatch(_ptr(data), _ptr(offsets), _ptr(lengths), len(offsets), _ptr(out),
                                        _ptr(out_offsets), flags, h), "BRB_Base64EncodeBatch")
     return out
 
 
-def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=None, stream=None, async_=False):
+def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=None, stream=None, async_=False,
+                        all_devices=False):
     """BRB_Base64DecodeBatch: returns out_lengths (uint32[n])."""
     n = len(offsets)
     if out_lengths is None:
@@ -485,7 +489,7 @@ def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=No
         else:
             out_lengths = np.zeros(n, np.uint32)
     _same_kind(text, offsets, lengths, out, out_offsets, out_lengths)
-    flags, h = _mode(text, stream, async_)
+    flags, h = _mode(text, stream, async_, all_devices)
     _check(lib().BRB_Base64DecodeBatch(_ptr(text), _ptr(offsets), _ptr(lengths), n, _ptr(out), _ptr(out_offsets),
                                        _ptr(out_lengths), flags, h), "BRB_Base64DecodeBatch")
     return out_lengths
@@ -495,6 +499,7 @@ def base64_decode_batch(text, offsets, lengths, out, out_offsets, out_lengths=No
 CRYPTO_FUNC_RC4, CRYPTO_FUNC_RC4_MD5 = 1, 2
 BATCHER_ZERO_COPY = 0x100
 BATCHER_PIPELINED = 0x200    # BRB_BATCHER_PIPELINED: two arenas, flush_async()
+BATCHER_ALL_DEVICES = 0x400  # BRB_BATCHER_ALL_DEVICES: connections partitioned over the devices
 OP_READ, OP_WRITE = 0, 1
 TransformDone = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32,
                                  ctypes.c_int)
@@ -536,7 +541,7 @@ class TransformBatcher:
     region per arena, since a running round's buffers must stay unchanged until delivered."""
 
     def __init__(self, max_conns: int, max_round_bytes: int, algo: int = CRYPTO_FUNC_RC4_MD5, zero_copy: bool = False,
-                 pipelined: bool = False):
+                 pipelined: bool = False, all_devices: bool = False):
         self._L = lib()
         n_reg = 2 if pipelined else 1
         self._regions = [HostRegion(max(max_round_bytes, 1)) for _ in range(n_reg)] if zero_copy else None
@@ -544,7 +549,8 @@ class TransformBatcher:
         self._used = 0
         self.h = self._L.BRB_TransformBatcherCreate(max_conns, max_round_bytes,
                                                     algo | (BATCHER_ZERO_COPY if zero_copy else 0) |
-                                                    (BATCHER_PIPELINED if pipelined else 0))
+                                                    (BATCHER_PIPELINED if pipelined else 0) |
+                                                    (BATCHER_ALL_DEVICES if all_devices else 0))
         if not self.h:
             raise RuntimeError("BRB_TransformBatcherCreate: " + self._L.BRB_CryptoGPU_LastError().decode())
 

@@ -398,6 +398,33 @@ std::vector<uint64_t> rebase(const uint64_t *offs, uint64_t n, uint64_t lo)
     return r;
 }
 
+// BRB_BATCH_ALL_DEVICES for the multi-range calls whose host-mode parts write a byte span back
+// (RC4 streams, frames, base64 outputs): part g stages and returns the span its ranges
+// [g n/G, (g+1) n/G) cover, so the split is taken only when those spans are pairwise disjoint --
+// otherwise a part would write back bytes of another part's ranges.  Streams of different
+// connections are disjoint by contract; ranges in submission order give disjoint spans.  Ranges
+// in any other order run on the calling thread's device (same results, one device).
+bool parts_disjoint(const uint64_t *offs, const uint32_t *lens, uint64_t n, uint64_t extra, const uint32_t *lens_out = nullptr)
+{
+    const int G = brb_host::split_parts();
+    if (G <= 1 || n < uint64_t(G))
+        return false;
+    std::vector<std::pair<uint64_t, uint64_t>> sp;
+    for (int g = 0; g < G; g++) {
+        const uint64_t a = n * uint64_t(g) / uint64_t(G), b = n * uint64_t(g + 1) / uint64_t(G);
+        uint64_t lo, hi;
+        if (!span_of(offs + a, lens_out ? lens_out + a : lens + a, b - a, extra, lo, hi))
+            return false;
+        if (hi > lo)
+            sp.push_back({lo, hi});
+    }
+    std::sort(sp.begin(), sp.end());
+    for (size_t i = 1; i < sp.size(); i++)
+        if (sp[i].first < sp[i - 1].second)
+            return false;
+    return true;
+}
+
 int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint64_t *offsets, const uint32_t *lengths,
                     uint64_t n, unsigned flags, void *stream)
 {
@@ -408,10 +435,17 @@ int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint
         set_err("NULL states, in, out, offsets or lengths");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n))
+    if (!items_ok(n) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES) {   // connections split over the devices, states with them
+        flags &= ~BRB_BATCH_ALL_DEVICES;
+        if (parts_disjoint(offsets, lengths, n, 0))
+            return brb_host::split_devices(n, [&](int, uint64_t lo, uint64_t hi) {
+                return rc4_crypt_batch(states + lo, in, out, offsets + lo, lengths + lo, hi - lo, flags, nullptr);
+            });
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
@@ -455,10 +489,18 @@ int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_
         set_err("NULL states, payload, offsets, lengths, salts, frames or frame_offsets");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n))
+    if (!items_ok(n) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES) {   // frames are written back: their spans must not interleave
+        flags &= ~BRB_BATCH_ALL_DEVICES;
+        if (parts_disjoint(frame_offsets, lengths, n, BRB_RC4MD5_HEADER))
+            return brb_host::split_devices(n, [&](int, uint64_t lo, uint64_t hi) {
+                return rc4md5_frame_batch(states + lo, payload, offsets + lo, lengths + lo, salts + lo, frames,
+                                          frame_offsets + lo, hi - lo, flags, nullptr);
+            });
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
@@ -503,10 +545,18 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
         set_err("NULL states, frames, out, offsets, lengths or valid");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n))
+    if (!items_ok(n) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES) {
+        flags &= ~BRB_BATCH_ALL_DEVICES;
+        if (parts_disjoint(offsets, lengths, n, 0))
+            return brb_host::split_devices(n, [&](int, uint64_t lo, uint64_t hi) {
+                return rc4md5_open_batch(states + lo, frames, out, offsets + lo, lengths + lo, hi - lo, valid + lo, flags,
+                                         nullptr);
+            });
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
@@ -549,10 +599,15 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
         set_err("NULL data, seg_offsets, seg_lengths, rec_first_seg or digests");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n_rec))
+    if (!items_ok(n_rec) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES)   // contiguous record ranges (segment lists with them), one per device
+        return brb_host::split_devices(n_rec, [&](int, uint64_t lo, uint64_t hi) {
+            return md5_segments(data, soff, slen, first + lo, hi - lo, static_cast<uint8_t *>(digests) + 16 * lo,
+                                flags & ~BRB_BATCH_ALL_DEVICES, nullptr);
+        });
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
@@ -653,10 +708,21 @@ int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t 
         set_err("NULL data, offsets, lengths, out, out_offsets or out_lengths");
         return BRB_BATCH_BADARG;
     }
-    if (!items_ok(n))
+    if (!items_ok(n) || !flags_ok(flags))
         return BRB_BATCH_BADARG;
     if (int ok = device_ok(); ok != BRB_BATCH_OK)
         return ok;
+    if (flags & BRB_BATCH_ALL_DEVICES) {   // outputs are written back: their spans must not interleave
+        flags &= ~BRB_BATCH_ALL_DEVICES;
+        std::vector<uint32_t> omax(n);
+        for (uint64_t i = 0; i < n; i++)
+            omax[i] = decode ? 3u * (lens[i] / 4) : 4u * ((lens[i] + 2) / 3);
+        if (parts_disjoint(ooffs, lens, n, 0, omax.data()))
+            return brb_host::split_devices(n, [&](int, uint64_t lo, uint64_t hi) {
+                return b64_batch(decode, in, offs + lo, lens + lo, hi - lo, out, ooffs + lo, olens ? olens + lo : nullptr,
+                                 flags, nullptr);
+            });
+    }
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
     auto launch = [&](const uint8_t *i, const uint64_t *o, const uint32_t *l, uint8_t *d, const uint64_t *oo,
@@ -933,7 +999,8 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
     } known[] = {{"rc4_sector", brb_opt::kRc4Sector, -1, 1},
                  {"var_line", brb_opt::kVarLine, 0, 1},
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
-                 {"var_sort", brb_opt::kVarSort, 0, 1}};
+                 {"var_sort", brb_opt::kVarSort, 0, 1},
+                 {"devices", brb_opt::kDevices, 0, 64}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

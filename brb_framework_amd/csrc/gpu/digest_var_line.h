@@ -66,9 +66,87 @@ BRB_DEV uint64_t wave_max64(uint64_t v)
     return v;
 }
 
+// ---- Bucketing of variable-length batches by length (SURVEY §7 "Hard parts").  A group of 64 lanes
+// runs to its longest record, so 64 consecutive records of lengths U[1000, 2000] cost ~1.33x their
+// mean.  Records are therefore grouped by length inside CHUNKS of CG groups (64 CG consecutive
+// records): the chunk's records are ranked by a bucket of their 2-block iteration count (stable:
+// equal buckets keep record order), and group j of the chunk takes ranks [64 j, 64 j + 64).  Every
+// wave that takes a group of the chunk computes the same ranking on its own -- ballots, mbcnt and
+// scalar popcounts are deterministic -- so no wave waits for another and the ticketed groups stay
+// as they are.  Digests go to each record's own slot (caller order).  Cost: one coalesced load of
+// the chunk's lengths, NB x CG ballots, one LDS scatter/gather per group (~200 instructions against
+// ~8 000 per group of 1 500-byte records).
+constexpr uint32_t kSortCG = 4;       // groups per chunk: 256 records
+constexpr uint32_t kSortNB = 8;       // buckets
+
+// Record of lane `lane` in group g (chunk c = g / kSortCG, j = g % kSortCG), or ~0 when that rank
+// holds no record (past n_rec).  `scratch`: this wave's 4 * 64 * kSortCG bytes of LDS.
+BRB_DEV uint64_t sorted_record(uint64_t g, uint32_t lane, const uint32_t *__restrict__ lens, uint64_t n_rec,
+                               uint32_t *scratch)
+{
+    const uint64_t c0 = (g / kSortCG) * kSortCG * 64;
+    const uint32_t j = uint32_t(g % kSortCG);
+    uint32_t it[kSortCG];
+    bool ok[kSortCG];
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < kSortCG; v++) {
+        const uint64_t idx = c0 + 64 * v + lane;
+        ok[v] = idx < n_rec;
+        const uint32_t len = ok[v] ? lens[idx] : 0u;
+        const uint32_t nb = (len >> 6) + ((len & 63) ? 1u : 0u);
+        it[v] = (nb >> 1) + (nb & 1);                          // the record's 2-block iterations
+        lo = ok[v] && it[v] < lo ? it[v] : lo;
+        hi = ok[v] && it[v] > hi ? it[v] : hi;
+    }
+    // wave-uniform range of the chunk's iteration counts
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t a = uint32_t(__shfl_xor(int(lo), m, 64)), b = uint32_t(__shfl_xor(int(hi), m, 64));
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    const uint32_t span = hi > lo ? hi - lo : 0u;
+    // bucket: iterations above the chunk's minimum, scaled onto kSortNB buckets when they span more
+    // (one float multiply; the same inputs give every wave the same buckets); no record: last
+    const float scale = span < kSortNB ? 1.0f : float(kSortNB - 1) / float(span);
+    uint32_t key[kSortCG], pos[kSortCG];
+#pragma unroll
+    for (uint32_t v = 0; v < kSortCG; v++) {
+        const uint32_t d = it[v] - lo;
+        const uint32_t q = uint32_t(float(d) * scale + 0.5f);
+        key[v] = !ok[v] ? kSortNB - 1 : (q < kSortNB ? q : kSortNB - 1);
+        pos[v] = 0;
+    }
+    uint32_t base = 0;                                         // uniform: records in buckets < k
+#pragma unroll
+    for (uint32_t k = 0; k < kSortNB; k++) {
+#pragma unroll
+        for (uint32_t v = 0; v < kSortCG; v++) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(key[v] == k);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+            pos[v] = key[v] == k ? base + below : pos[v];
+            base += uint32_t(__builtin_popcountll(m));
+        }
+    }
+    // rank -> record through the wave's scratch
+#pragma unroll
+    for (uint32_t v = 0; v < kSortCG; v++)
+        scratch[pos[v]] = ok[v] ? 64 * v + lane : 0xFFFFFFFFu;
+    __builtin_amdgcn_s_waitcnt(0xC07F);                        // lgkmcnt(0): the scatter has landed
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t e = scratch[64 * j + lane];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    return e == 0xFFFFFFFFu ? ~uint64_t(0) : c0 + e;
+}
+
 // FIXED: record r = data[r * rec_len .. + rec_len) (offs / lens unused) -- fixed-stride batches
 // whose records are not 4-byte aligned, which digest_line_kernel's dword window cannot take.
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool FIXED = false>
+// SORT: groups bucketed by length inside chunks of kSortCG groups (sorted_record).
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool FIXED = false, bool SORT = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const uint8_t *__restrict__ data,
                                                                         const uint64_t *__restrict__ offs,
                                                                         const uint32_t *__restrict__ lens,
@@ -78,6 +156,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
     constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
     constexpr uint32_t OOB = 0x80000000u;                      // a voffset past every descriptor's range
     __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
+    __shared__ uint32_t sort_scratch[SORT ? WAVES * 64 * kSortCG : 1];
     __shared__ uint32_t next_ticket;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -103,6 +182,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
     // ---- one group's layout (Grp): this lane's record, and the group's descriptor and DMA lanes
     struct Grp {
         uint64_t a;          // address of this lane's record
+        uint64_t r;          // its index (the digest's slot), ~0 for none
         uint32_t len;
         uint32_t K;          // 2-block iterations of the group (its longest record)
         bool line;           // false: the group's lines span >= 2 GiB, use digest_lane
@@ -110,12 +190,23 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
         uint32_t vq[8];      // DMA voffsets of rows 8q + lane / 8 (line 0 relative to the descriptor)
         uint32_t lq[8];      // lines of those rows' records
     };
-    auto setup = [&](uint64_t g, Grp &G) {
-        const uint64_t r0 = g * 64;
-        const uint32_t last = uint32_t(n_rec - r0 < 64 ? n_rec - r0 - 1 : 63);
-        const uint64_t r = r0 + (lane < last ? lane : last);
+    // Record of this lane in group g: caller order (64 g + lane), or, for SORT groups past the first
+    // round of tickets (g >= first_sorted: whole chunks, since every wave of the grid takes one group
+    // of the first round and 8 x gridDim.x is a multiple of kSortCG), the length-bucketed order of
+    // sorted_record.  The first round stays in caller order so that no wave waits for a ranking
+    // before its first DMA; a later group's ranking is computed while the group before it runs.
+    // ~0: no record (past n_rec).
+    const uint64_t first_sorted = uint64_t(WAVES) * gridDim.x;
+    auto record_of = [&](uint64_t g) -> uint64_t {
+        if (SORT && g >= first_sorted && g < n_groups)
+            return sorted_record(g, lane, lens, n_rec, sort_scratch + wv * (64 * kSortCG));
+        return g * 64 + lane < n_rec ? g * 64 + lane : ~uint64_t(0);
+    };
+    auto setup = [&](uint64_t g, uint64_t rec, Grp &G) {
+        const uint64_t r = rec != ~uint64_t(0) ? rec : uniform64(g * 64);   // no record: empty, valid offset
+        G.r = rec;
         G.a = dbase + (FIXED ? r * rec_len : offs[r]);
-        G.len = FIXED ? rec_len : lens[r];
+        G.len = FIXED ? rec_len : (rec != ~uint64_t(0) ? lens[r] : 0u);
         const uint64_t line = G.a & ~uint64_t(127);
         const uint32_t lines = G.len ? uint32_t(((G.a & 127) + G.len + 127) >> 7) : 0u;
         const uint32_t nblk = (G.len >> 6) + ((G.len & 63) ? 1u : 0u);
@@ -220,17 +311,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
     };
 
     Grp G, Gn;
-    setup(g, G);
+    setup(g, record_of(g), G);
     start(G);
     __builtin_amdgcn_sched_barrier(0);
     for (;;) {
         const uint64_t gn = take();
-        const uint64_t r = g * 64 + lane;
+        const uint64_t rn = record_of(gn);                     // ranking of the next group, if sorted
+        const uint64_t r = G.r;
         typename Alg::State st;
         if (!G.line) {
             st = digest_lane<Alg>(reinterpret_cast<const uint8_t *>(G.a), G.len);
             if (gn < n_groups) {
-                setup(gn, Gn);
+                setup(gn, rn, Gn);
                 start(Gn);
             }
         } else {
@@ -250,7 +342,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
                 if (k < K) {
                     issue(G, k + 1, refill_slot);
                 } else if (gn < n_groups) {
-                    setup(gn, Gn);
+                    setup(gn, rn, Gn);
                     start(Gn);
                 }
                 const uint32_t b = 2 * k - 2;
@@ -267,7 +359,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
             if (K == 0) {                                      // every record of the group is empty
                 brb_dma::wait_vmcnt<0>();
                 if (gn < n_groups) {
-                    setup(gn, Gn);
+                    setup(gn, rn, Gn);
                     start(Gn);
                 }
             }
@@ -293,7 +385,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
                 Alg::finish(st, wt, t, G.len);
             }
         }
-        if (r < n_rec)
+        if (r != ~uint64_t(0))
             Alg::template store<OUT_ALIGNED>(out, r, st);
         g = gn;
         if (g >= n_groups)
@@ -310,7 +402,14 @@ hipError_t launch_var_line(const uint8_t *data, const uint64_t *offs, const uint
     constexpr int W = 8;
     const uint64_t groups = (n_rec + 63) / 64;
     const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
-    if (out_al)
+    // bucketing pays only where waves take several groups (with one group per wave the batch's
+    // longest record sets the time whatever the grouping): groups past the first round of tickets
+    const bool sort = brb_opt::get(brb_opt::kVarSort) != 0 && groups > uint64_t(g) * W;
+    if (sort && out_al)
+        digest_var_line_kernel<Alg, W, true, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
+    else if (sort)
+        digest_var_line_kernel<Alg, W, false, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
+    else if (out_al)
         digest_var_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
     else
         digest_var_line_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);

@@ -32,10 +32,13 @@ int digest_fixed(FixedLauncher launch, size_t dig_len, const uint8_t *data, uint
 int blowfish(const BRB_BLOWFISH_CTX *ctx, uint64_t *words, uint64_t n_items, bool decrypt, unsigned flags,
              hipStream_t s);
 
-// Runs part(dev, lo, hi) for the contiguous ranges [g*n/G, (g+1)*n/G) of n items over the G visible
-// devices, concurrently (one persistent worker thread per device, current device = dev), and
+// Runs part(dev, lo, hi) for the contiguous ranges [g*n/G, (g+1)*n/G) of n items over G parts,
+// concurrently (one persistent worker thread per part, current device = dev = part_device(g)), and
 // returns BRB_BATCH_OK or the first failing part's code with "device g: <reason>" in LastError.
+// G = the visible devices, or the "devices" test option (parts mapped onto the visible devices).
 int split_devices(uint64_t n, const std::function<int(int dev, uint64_t lo, uint64_t hi)> &part);
+int split_parts();                 // G
+int part_device(int g);            // the device of part g
 
 // Destroys the calling thread's pipeline streams and events (BRB_CryptoGPU_ThreadCleanup).
 void release_thread_pipes();

@@ -23,6 +23,7 @@
 #include "api_util.h"
 #include "brb_kernels.h"
 #include "host_pipe.h"
+#include "test_options.h"
 
 namespace {
 
@@ -61,9 +62,9 @@ class Pending;
 void post_d2h(int dev, Pending &pending, hipStream_t s_out, hipEvent_t ev, void *dst, const void *src, size_t bytes);
 
 // ---- persistent worker threads -------------------------------------------------------------------
-// One per (device, role): role 0 runs a device's share of an all-devices split, role 1 issues D2H
-// copies.  They live for the whole process (never joined: nothing may wait on a GPU runtime that is
-// being torn down at exit).
+// One per (part or device, role): role 0 runs part g of an all-devices split on device g % count,
+// role 1 issues a device's D2H copies.  They live for the whole process (never joined: nothing may
+// wait on a GPU runtime that is being torn down at exit).
 class Worker {
 public:
     explicit Worker(int dev) : dev_(dev) { std::thread([this] { run(); }).detach(); }
@@ -97,12 +98,13 @@ private:
     std::deque<std::function<void()>> q_;
 };
 
-Worker &worker(int dev, int role)
+// `idx`: the part (role 0) or the device (role 1); the thread runs on device `dev`.
+Worker &worker(int idx, int role, int dev)
 {
     static std::mutex mu;
     static auto *pool = new std::vector<Worker *>;   // intentionally never destroyed
     std::lock_guard<std::mutex> lk(mu);
-    const size_t i = size_t(dev) * 2 + size_t(role);
+    const size_t i = size_t(idx) * 2 + size_t(role);
     if (pool->size() <= i)
         pool->resize(i + 1, nullptr);
     if (!(*pool)[i])
@@ -152,7 +154,7 @@ private:
 void post_d2h(int dev, Pending &pending, hipStream_t s_out, hipEvent_t ev, void *dst, const void *src, size_t bytes)
 {
     pending.add();
-    worker(dev, 1).post([=, &pending] {
+    worker(dev, 1, dev).post([=, &pending] {
         hipError_t x;
         int r = BRB_BATCH_OK;
         std::string why;
@@ -352,9 +354,21 @@ void release_thread_pipes()
     t_pipes.release();
 }
 
+int split_parts()
+{
+    const int forced = brb_opt::get(brb_opt::kDevices);
+    return forced > 0 ? forced : brb_api::device_count();
+}
+
+int part_device(int g)
+{
+    const int n = brb_api::device_count();
+    return n > 0 ? g % n : 0;
+}
+
 int split_devices(uint64_t n, const std::function<int(int, uint64_t, uint64_t)> &part)
 {
-    const int G = brb_api::device_count();
+    const int G = split_parts();
     if (G <= 1 || n < uint64_t(G)) {
         DeviceGuard g(0);
         if (g.error() != hipSuccess)
@@ -370,10 +384,11 @@ int split_devices(uint64_t n, const std::function<int(int, uint64_t, uint64_t)> 
     for (int g = 0; g < G; g++) {
         const uint64_t lo = n * uint64_t(g) / uint64_t(G), hi = n * uint64_t(g + 1) / uint64_t(G);
         pending.add();
-        worker(g, 0).post([&, g, lo, hi] {
+        const int dev = part_device(g);
+        worker(g, 0, dev).post([&, g, dev, lo, hi] {
             brb_api::clear_err();
-            DeviceGuard dg{g};                         // the worker selected g at start; a failure there shows here
-            res[g].rc = dg.error() != hipSuccess ? fail_hip("hipSetDevice", dg.error()) : part(g, lo, hi);
+            DeviceGuard dg{dev};                       // the worker selected dev at start; a failure there shows here
+            res[g].rc = dg.error() != hipSuccess ? fail_hip("hipSetDevice", dg.error()) : part(dev, lo, hi);
             if (res[g].rc != BRB_BATCH_OK)
                 res[g].err = brb_api::t_err;
             pending.done(BRB_BATCH_OK, std::string());

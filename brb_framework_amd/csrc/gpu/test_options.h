@@ -12,10 +12,13 @@ enum Opt {
     kVarLine = 1,       // 1: variable-length digests on the line kernel; 0: per-lane kernel
     kFixedVarLine = 2,  // 1: byte-aligned fixed-stride records on the var-line kernel; 0: record-relative
     kVarSort = 3,       // 1: variable-length batches bucketed by block count; 0: caller order
-    kCount = 4
+    kDevices = 4,       // 0: BRB_BATCH_ALL_DEVICES / all-devices batchers use every visible device;
+                        // k > 0: they split into k parts, part g on device g % (visible devices) --
+                        // the concurrent multi-device paths exercised on a one-GPU box
+    kCount = 5
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -27,6 +27,7 @@
 #include "api_util.h"
 #include "brb_crypto.h"
 #include "brb_kernels.h"
+#include "host_pipe.h"
 
 using brb_api::DeviceGuard;
 using brb_api::fail_hip;
@@ -138,7 +139,22 @@ struct Chunk {
     uint64_t gen = 0;
     uint64_t slot = 0, slot_end = 0, in = 0, in_end = 0, out = 0, out_end = 0;
 };
-thread_local Chunk t_chunk;
+// One entry per round this thread submits into: an all-devices batcher's Read/Write alternate
+// between its parts' rounds, and with a single entry every switch abandoned the chunk just taken
+// (its slots became holes and a part's round reported full after a few dozen buffers).
+constexpr int kChunks = 16;
+thread_local Chunk t_chunks[kChunks];
+thread_local unsigned t_chunk_next = 0;
+
+Chunk &chunk_for(uint64_t gen)
+{
+    for (Chunk &c : t_chunks)
+        if (c.gen == gen)
+            return c;
+    Chunk &c = t_chunks[t_chunk_next++ % kChunks];   // oldest entry: its unused slots stay holes
+    c = Chunk{gen, 0, 0, 0, 0, 0, 0};
+    return c;
+}
 constexpr uint64_t kChunkSlots = 64, kChunkBytes = 128 << 10;
 
 // One round's arenas and bookkeeping.  A pipelined batcher (BRB_BATCHER_PIPELINED) owns two, so the
@@ -209,9 +225,17 @@ struct BRB_TransformBatcher {
     uint64_t max_items = 0;    // buffers per round: 4 per connection on average
     Round r[2];
     std::vector<uint8_t> enabled;
+    // BRB_BATCHER_ALL_DEVICES: the connections are partitioned over G sub-batchers, connection c
+    // in sub c % G as its connection c / G, sub g on device g % (visible devices); this object then
+    // only routes (no collective -- a connection's states live on its device).
+    std::vector<BRB_TransformBatcher *> subs;
 
     ~BRB_TransformBatcher()
     {
+        for (BRB_TransformBatcher *sb : subs)
+            delete sb;
+        if (!subs.empty())
+            return;
         DeviceGuard g(dev);
         for (hipStream_t q : {s_h2d, s_d2h, stream})
             if (q)
@@ -254,6 +278,34 @@ extern "C" {
 BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t max_round_bytes, int algo)
 {
     brb_api::clear_err();
+    if (algo & BRB_BATCHER_ALL_DEVICES) {
+        algo &= ~BRB_BATCHER_ALL_DEVICES;
+        if (brb_api::device_ok() != BRB_BATCH_OK)
+            return nullptr;
+        const int G = brb_host::split_parts();
+        if (G > 1 && max_conns >= uint32_t(G)) {
+            auto *m = new BRB_TransformBatcher;
+            m->max_conns = max_conns;
+            m->algo = algo;
+            for (int g = 0; g < G; g++) {
+                DeviceGuard dg(brb_host::part_device(g));
+                BRB_TransformBatcher *sb = dg.error() == hipSuccess
+                                               ? BRB_TransformBatcherCreate((max_conns - uint32_t(g) + uint32_t(G) - 1) / uint32_t(G),
+                                                                            max_round_bytes, algo)
+                                               : nullptr;
+                if (!sb) {
+                    if (dg.error() != hipSuccess)
+                        fail_hip("hipSetDevice", dg.error());
+                    const std::string why = brb_api::t_err;
+                    delete m;
+                    set_err("all-devices batcher, part %d: %s", g, why.c_str());
+                    return nullptr;
+                }
+                m->subs.push_back(sb);
+            }
+            return m;
+        }
+    }
     const bool zc = (algo & BRB_BATCHER_ZERO_COPY) != 0;
     const bool pipelined = (algo & BRB_BATCHER_PIPELINED) != 0;
     algo &= ~(BRB_BATCHER_ZERO_COPY | BRB_BATCHER_PIPELINED);
@@ -318,6 +370,8 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
         set_err("bad batcher, key or connection id");
         return BRB_BATCH_BADARG;
     }
+    if (!b->subs.empty())
+        return BRB_TransformBatcherEnable(b->subs[conn % b->subs.size()], conn / uint32_t(b->subs.size()), key, key_sz);
     BRB_RC4_State st;
     memset(&st, 0, sizeof(st));              // ev_kq_aio_transform.c:78 memset of the crypto states
     BRB_RC4_Init(&st, static_cast<const unsigned char *>(key), key_sz);
@@ -337,6 +391,8 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
 static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *data, uint32_t len, uint64_t salt)
 {
     brb_api::clear_err();
+    if (b && !b->subs.empty() && conn < b->max_conns)
+        return submit(b->subs[conn % b->subs.size()], conn / uint32_t(b->subs.size()), op, data, len, salt);
     if (!b || (!data && len) || conn >= b->max_conns || !b->enabled[conn]) {
         set_err("bad batcher, data or connection (not enabled?)");
         return BRB_BATCH_BADARG;
@@ -346,10 +402,8 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
     // Slot order is delivery order.  A thread's slots and bytes come from its own chunks, taken in
     // increasing order, so the buffers of a connection (owned by one thread) keep their order.
     // Slots of a chunk left unused stay holes; the metadata arrays fit max_items slots.
-    Chunk &k = t_chunk;
     const uint64_t gen = R.gen.load(std::memory_order_relaxed);
-    if (k.gen != gen)
-        k = Chunk{gen, 0, 0, 0, 0, 0, 0};
+    Chunk &k = chunk_for(gen);
     uint64_t got;
     if (k.slot == k.slot_end) {
         const uint64_t s0 = take(R.n_slots, b->max_items, 1, kChunkSlots, &got);
@@ -625,6 +679,104 @@ static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDon
     return n;
 }
 
+// ---- Flush / FlushAsync in phases, so that an all-devices batcher can enqueue every device's
+// round before it waits for any of them (the devices run concurrently; the callbacks still come on
+// the calling thread, device by device, each device's buffers in submission order).
+//   Flush:      deliver the round FlushAsync left running (pipelined) | launch the current round |
+//               deliver it
+//   FlushAsync: launch the current round and switch arenas | deliver the previous round
+struct Phase {
+    BRB_TransformBatcher *b;
+    BRB_TransformDone done;
+    void *user;
+    Round *prev = nullptr;     // FlushAsync: the round to deliver after the launches
+    int64_t n = 0;             // buffers delivered
+    bool dropped = false;
+    bool failed = false;       // hipSetDevice failed: the round stays pending
+};
+
+// the batcher's connection ids -> the caller's (all-devices: sub g's connection c is c * G + g)
+struct Tramp {
+    BRB_TransformDone done;
+    void *user;
+    uint32_t G, g;
+    static void call(void *u, uint32_t conn, int op, const void *out, uint32_t len, int valid)
+    {
+        const Tramp *t = static_cast<const Tramp *>(u);
+        t->done(t->user, conn * t->G + t->g, op, out, len, valid);
+    }
+};
+
+static void phase_deliver(Phase &p, Round &R)
+{
+    if (!R.in_flight)
+        return;
+    DeviceGuard g(p.b->dev);
+    const int64_t n = deliver_round(p.b, R, p.done, p.user);
+    if (n < 0)
+        p.dropped = true;
+    else
+        p.n += n;
+}
+
+static void phase_launch(Phase &p, bool async)
+{
+    BRB_TransformBatcher *b = p.b;
+    DeviceGuard g(b->dev);
+    if (g.error() != hipSuccess) {
+        fail_hip("hipSetDevice", g.error());
+        p.failed = true;
+        return;
+    }
+    Round &R = b->r[b->cur];
+    p.prev = async && b->n_rounds == 2 ? &b->r[b->cur ^ 1] : nullptr;
+    if (collect(b, R) == 0)
+        R.reset();
+    else if (launch_round(b, R, p.done, p.user) != BRB_BATCH_OK)   // dropped: its callbacks have fired
+        p.dropped = true;
+    if (async && b->n_rounds == 2 && R.in_flight)
+        b->cur ^= 1;        // Read/Write now fill the other arena (the previous round's, once delivered)
+}
+
+static int64_t flush_all(BRB_TransformBatcher *b, BRB_TransformDone done, void *user, bool async)
+{
+    std::vector<BRB_TransformBatcher *> parts = b->subs;
+    if (parts.empty())
+        parts.push_back(b);
+    const uint32_t G = uint32_t(parts.size());
+    std::vector<Tramp> tr(G);
+    std::vector<Phase> ph;
+    for (uint32_t g = 0; g < G; g++) {
+        tr[g] = Tramp{done, user, G, g};
+        ph.push_back(Phase{parts[g], done ? (b->subs.empty() ? done : &Tramp::call) : nullptr,
+                           b->subs.empty() ? user : static_cast<void *>(&tr[g])});
+    }
+    const bool pipelined = parts[0]->n_rounds == 2;
+    if (!async || !pipelined) {
+        if (pipelined)
+            for (Phase &p : ph)   // the rounds FlushAsync left running come first
+                phase_deliver(p, p.b->r[p.b->cur ^ 1]);
+        for (Phase &p : ph)
+            phase_launch(p, false);
+        for (Phase &p : ph)
+            phase_deliver(p, p.b->r[p.b->cur]);
+    } else {
+        for (Phase &p : ph)
+            phase_launch(p, true);
+        for (Phase &p : ph)
+            if (p.prev)
+                phase_deliver(p, *p.prev);
+    }
+    int64_t total = 0;
+    bool dropped = false, failed = false;
+    for (const Phase &p : ph) {
+        total += p.n;
+        dropped |= p.dropped;
+        failed |= p.failed;
+    }
+    return dropped ? BRB_BATCH_DROPPED : failed ? BRB_BATCH_NOT_DONE : total;
+}
+
 extern "C" {
 
 int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
@@ -634,29 +786,7 @@ int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone don
         set_err("NULL batcher");
         return BRB_BATCH_BADARG;
     }
-    DeviceGuard g(b->dev);
-    hipError_t e;
-    if ((e = g.error()) != hipSuccess)
-        return fail_hip("hipSetDevice", e);
-    int64_t total = 0;
-    bool dropped = false;
-    Round &prev = b->r[b->cur ^ (b->n_rounds - 1)];
-    if (b->n_rounds == 2 && prev.in_flight) {   // the round FlushAsync left running comes first
-        const int64_t n = deliver_round(b, prev, done, user);
-        if (n < 0)
-            dropped = true;                      // the current round still runs below
-        else
-            total += n;
-    }
-    Round &R = b->r[b->cur];
-    if (collect(b, R) == 0) {
-        R.reset();
-        return dropped ? BRB_BATCH_DROPPED : total;
-    }
-    if (launch_round(b, R, done, user) != BRB_BATCH_OK)
-        return BRB_BATCH_DROPPED;
-    const int64_t n = deliver_round(b, R, done, user);
-    return n < 0 || dropped ? BRB_BATCH_DROPPED : total + n;
+    return flush_all(b, done, user, false);
 }
 
 int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDone done, void *user)
@@ -666,26 +796,7 @@ int64_t BRB_TransformBatcherFlushAsync(BRB_TransformBatcher *b, BRB_TransformDon
         set_err("NULL batcher");
         return BRB_BATCH_BADARG;
     }
-    if (b->n_rounds == 1)
-        return BRB_TransformBatcherFlush(b, done, user);
-    DeviceGuard g(b->dev);
-    hipError_t e;
-    if ((e = g.error()) != hipSuccess)
-        return fail_hip("hipSetDevice", e);
-    Round &R = b->r[b->cur], &prev = b->r[b->cur ^ 1];
-    // enqueue this round first so the GPU has it while the previous round's callbacks run; a failed
-    // one is dropped (its callbacks fire), and the previous round is still delivered below
-    bool dropped = false;
-    if (collect(b, R) == 0)
-        R.reset();
-    else if (launch_round(b, R, done, user) != BRB_BATCH_OK)
-        dropped = true;
-    if (R.in_flight)
-        b->cur ^= 1;   // Read/Write now fill the other arena (the previous round's, once delivered)
-    int64_t n = 0;
-    if (prev.in_flight)
-        n = deliver_round(b, prev, done, user);
-    return n < 0 || dropped ? BRB_BATCH_DROPPED : n;
+    return flush_all(b, done, user, true);
 }
 
 int BRB_TransformBatcherInjectFault(BRB_TransformBatcher *b, int launch)
@@ -696,6 +807,8 @@ int BRB_TransformBatcherInjectFault(BRB_TransformBatcher *b, int launch)
         return BRB_BATCH_BADARG;
     }
     b->fault_launch = launch;
+    for (BRB_TransformBatcher *sb : b->subs)
+        sb->fault_launch = launch;
     return BRB_BATCH_OK;
 }
 
@@ -712,7 +825,7 @@ int BRB_CryptoGPU_HostRegister(void *p, uint64_t len)
     }
     if (int ok = brb_api::device_ok(); ok != BRB_BATCH_OK)
         return ok;
-    hipError_t e = hipHostRegister(p, len, hipHostRegisterMapped);
+    hipError_t e = hipHostRegister(p, len, hipHostRegisterMapped | hipHostRegisterPortable);   // every device
     if (e != hipSuccess)
         return fail_hip("hipHostRegister", e);
     void *dp = nullptr;
@@ -750,6 +863,8 @@ int BRB_TransformBatcherGetState(BRB_TransformBatcher *b, uint32_t conn, int op,
         set_err("bad batcher, connection or op");
         return BRB_BATCH_BADARG;
     }
+    if (!b->subs.empty())
+        return BRB_TransformBatcherGetState(b->subs[conn % b->subs.size()], conn / uint32_t(b->subs.size()), op, out);
     DeviceGuard g(b->dev);
     hipError_t e;
     if ((e = g.error()) != hipSuccess ||

@@ -60,3 +60,9 @@ def gen_words(seed: int, n_words: int, r0: int = 0) -> np.ndarray:
 def shard(n: int, rank: int, world: int) -> tuple:
     """Contiguous record range of `rank`: [rank*n/world, (rank+1)*n/world)."""
     return (n * rank) // world, (n * (rank + 1)) // world
+
+
+def conn_part(conn: int, parts: int) -> tuple:
+    """Part and local connection id of `conn` in an all-devices transform batcher
+    (BRB_BATCHER_ALL_DEVICES): connection c lives on part c % G as its connection c // G."""
+    return conn % parts, conn // parts

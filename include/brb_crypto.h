@@ -117,12 +117,15 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
                                       is device memory (HBM-resident); nothing crosses PCIe       */
 #define BRB_BATCH_ASYNC     0x2u   /* with BRB_BATCH_DEVICE: enqueue on `hip_stream` and return
                                       without waiting; the caller synchronises the stream         */
-#define BRB_BATCH_ALL_DEVICES 0x4u /* host mode only (BRB_MD5BatchFixed, BRB_MD5Batch,
-                                      BrbSha1_BatchFixed, BrbSha1_Batch, BRB_Blowfish_*Batch):
-                                      split the records (blocks) into contiguous ranges
-                                      [g*n/G, (g+1)*n/G), one per visible device g < G, run them
-                                      concurrently and return when all are done (SURVEY §8(e):
-                                      no collective).  With BRB_BATCH_DEVICE: -1.                   */
+#define BRB_BATCH_ALL_DEVICES 0x4u /* host mode only (every batch call except MemBuffer):
+                                      split the records (blocks, streams, packs) into contiguous
+                                      ranges [g*n/G, (g+1)*n/G), one per visible device g < G, run
+                                      them concurrently and return when all are done (SURVEY §8(e):
+                                      no collective); the RC4 states go with their streams.  Calls
+                                      that write a byte span back (RC4, frames, base64 outputs)
+                                      split only when the ranges' spans do not interleave across
+                                      parts (ranges in submission order); otherwise they run on the
+                                      calling thread's device.  With BRB_BATCH_DEVICE: -1.           */
 
 /* Device mode: `hip_stream` is a hipStream_t (NULL = the legacy default stream of the current
  * device) and the work runs on the caller's current HIP device (BRB_CryptoGPU_SetDevice,
@@ -256,6 +259,14 @@ int BRB_RC4MD5_OpenBatch(BRB_RC4_State *states, const void *frames, void *out, c
 /* OR into `algo` at Create: pipelined rounds.  The batcher owns two rounds' arenas, so the loop fills
  * round k+1 while the GPU runs round k (BRB_TransformBatcherFlushAsync).  Twice the arena memory. */
 #define BRB_BATCHER_PIPELINED     0x200
+/* OR into `algo` at Create: all devices (the daemon's multi-threaded engine spreading connections,
+ * ev_kq_base.c:95).  Connection c lives on device c % G (G = visible devices) with its read and
+ * write states; Read/Write/Enable/GetState route by connection, and one Flush / FlushAsync enqueues
+ * every device's round before it waits for any, so the devices run concurrently.  Callbacks come on
+ * the calling thread, device by device: each connection's buffers keep their order, buffers of
+ * connections on different devices are not interleaved in submission order.  With one device (or
+ * max_conns < G) this is a plain batcher. */
+#define BRB_BATCHER_ALL_DEVICES   0x400
 typedef struct BRB_TransformBatcher BRB_TransformBatcher;
 typedef void (*BRB_TransformDone)(void *user, uint32_t conn, int op, const void *out, uint32_t out_len, int valid);
 /* `valid` of a buffer whose round was dropped (out = NULL, out_len = 0): see Flush. */

@@ -46,6 +46,9 @@ def lib() -> ctypes.CDLL:
             "orc_sha1_batch_fixed": (None, [vp, ctypes.c_uint32, u64, vp, ctypes.c_int]),
             "orc_md5_batch": (None, [vp, vp, vp, u64, vp]),
             "orc_sha1_batch": (None, [vp, vp, vp, u64, vp]),
+            "orc_md5_batch_mt": (None, [vp, vp, vp, u64, vp, ctypes.c_int]),
+            "orc_sha1_batch_mt": (None, [vp, vp, vp, u64, vp, ctypes.c_int]),
+            "orc_rc4_crypt_batch": (None, [vp, vp, vp, vp, u64, ctypes.c_int]),
             "orc_rc4_init": (None, [vp, vp, ctypes.c_int]),
             "orc_rc4_crypt": (None, [vp, vp, vp, ctypes.c_int]),
             "orc_rc4md5_frame": (None, [vp, vp, u64, u64, vp]),
@@ -98,20 +101,28 @@ def sha1_batch_fixed(data: np.ndarray, rec_len: int, n: int, threads: int = 1) -
     return out
 
 
-def md5_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+def md5_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1) -> np.ndarray:
     offsets = np.ascontiguousarray(offsets, np.uint64)
     lengths = np.ascontiguousarray(lengths, np.uint32)
     out = np.empty((len(offsets), 16), np.uint8)
-    lib().orc_md5_batch(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out))
+    lib().orc_md5_batch_mt(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out), threads)
     return out
 
 
-def sha1_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.ndarray:
+def sha1_batch(data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1) -> np.ndarray:
     offsets = np.ascontiguousarray(offsets, np.uint64)
     lengths = np.ascontiguousarray(lengths, np.uint32)
     out = np.empty((len(offsets), 20), np.uint8)
-    lib().orc_sha1_batch(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out))
+    lib().orc_sha1_batch_mt(_p(data), _p(offsets), _p(lengths), len(offsets), _p(out), threads)
     return out
+
+
+def rc4_crypt_batch(states: np.ndarray, data: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+                    threads: int = 1) -> None:
+    """BRB_RC4_Crypt in place on every stream; states (n, 264) uint8 advanced in place."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lengths = np.ascontiguousarray(lengths, np.uint32)
+    lib().orc_rc4_crypt_batch(_p(states), _p(data), _p(offsets), _p(lengths), len(offsets), threads)
 
 
 class Md5Ctx(ctypes.Structure):

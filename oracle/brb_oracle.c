@@ -507,6 +507,54 @@ void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *le
     for (uint64_t r = 0; r < n; r++) orc_sha1(data + off[r], len[r], out20 + 20 * r);
 }
 
+/* The same on n_threads pthreads over contiguous record ranges (bench.py's cpu_baseline of the
+ * variable-length legs). */
+typedef struct {
+    const uint8_t *data;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t r0, r1;
+    uint8_t *out;
+    int sha;
+} var_job;
+
+static void *var_worker(void *arg)
+{
+    var_job *j = (var_job *)arg;
+    if (j->sha) orc_sha1_batch(j->data, j->off + j->r0, j->len + j->r0, j->r1 - j->r0, j->out + 20 * j->r0);
+    else orc_md5_batch(j->data, j->off + j->r0, j->len + j->r0, j->r1 - j->r0, j->out + 16 * j->r0);
+    return NULL;
+}
+
+static void var_run(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out,
+                    int n_threads, int sha)
+{
+    pthread_once(&md5_once, md5_tables);
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    pthread_t th[256];
+    var_job jobs[256];
+    for (int t = 0; t < n_threads; t++) {
+        jobs[t] = (var_job){data, off, len, n * (uint64_t)t / (uint64_t)n_threads,
+                            n * (uint64_t)(t + 1) / (uint64_t)n_threads, out, sha};
+    }
+    if (n_threads == 1) { var_worker(&jobs[0]); return; }
+    for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, var_worker, &jobs[t]);
+    for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_md5_batch_mt(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16,
+                      int n_threads)
+{
+    var_run(data, off, len, n, out16, n_threads, 0);
+}
+
+void orc_sha1_batch_mt(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out20,
+                       int n_threads)
+{
+    var_run(data, off, len, n, out20, n_threads, 1);
+}
+
 /* =========================================================================================== */
 /* RC4 -- libbrb_core/crypto/rc4.c                                                               */
 /* =========================================================================================== */
@@ -621,6 +669,22 @@ static void rc4_run(rc4_job proto, uint64_t n, int n_threads, void *(*fn)(void *
     if (n_threads == 1) { fn(&jobs[0]); return; }
     for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, fn, &jobs[t]);
     for (int t = 0; t < n_threads; t++) pthread_join(th[t], NULL);
+}
+
+static void *rc4_crypt_worker(void *arg)
+{
+    rc4_job *j = (rc4_job *)arg;
+    for (uint64_t r = j->r0; r < j->r1; r++)
+        orc_rc4_crypt(&j->s[r], j->frames + j->off[r], j->frames + j->off[r], (int)j->len[r]);
+    return NULL;
+}
+
+/* BRB_RC4_Crypt in place on n streams (stream r = data[off[r] .. + len[r]) with state s[r]). */
+void orc_rc4_crypt_batch(orc_rc4_state *s, uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n,
+                         int n_threads)
+{
+    rc4_job p = {s, NULL, data, off, NULL, NULL, len, NULL, 0, 0};
+    rc4_run(p, n, n_threads, rc4_crypt_worker);
 }
 
 void orc_rc4md5_frame_batch(orc_rc4_state *s, const uint8_t *payload, const uint64_t *off, const uint32_t *len,

@@ -106,6 +106,8 @@ void orc_rc4_crypt(orc_rc4_state *s, const unsigned char *in, unsigned char *out
 void orc_rc4md5_frame(orc_rc4_state *s, const uint8_t *payload, uint64_t len, uint64_t salt, uint8_t *frame);
 int orc_rc4md5_open(orc_rc4_state *s, uint8_t *frame, uint64_t frame_len);
 /* n connections (pthreads over contiguous connection ranges; bench.py's cpu_baseline) */
+void orc_rc4_crypt_batch(orc_rc4_state *s, uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n,
+                         int n_threads);
 void orc_rc4md5_frame_batch(orc_rc4_state *s, const uint8_t *payload, const uint64_t *off, const uint32_t *len,
                             const uint64_t *salts, uint8_t *frames, const uint64_t *foff, uint64_t n, int n_threads);
 void orc_rc4md5_open_batch(orc_rc4_state *s, uint8_t *frames, const uint64_t *off, const uint32_t *len, uint64_t n,
@@ -124,6 +126,10 @@ void orc_md5_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint
 void orc_sha1_batch_fixed(const uint8_t *data, uint32_t rec_len, uint64_t n, uint8_t *out20, int n_threads);
 void orc_md5_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16);
 void orc_sha1_batch(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out20);
+void orc_md5_batch_mt(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out16,
+                      int n_threads);
+void orc_sha1_batch_mt(const uint8_t *data, const uint64_t *off, const uint32_t *len, uint64_t n, uint8_t *out20,
+                       int n_threads);
 
 /* ---- Deterministic input generator --------------------------------------
  * byte(r, k) = byte (k mod 8), little-endian, of splitmix64(seed ^ (r * 0x9E3779B97F4A7C15) ^ (k >> 3))

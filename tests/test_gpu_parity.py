@@ -346,6 +346,44 @@ def test_variable_records_line_kernel(brb, orc, torch_dev, n, max_len, seed):
     assert np.array_equal(brb.md5_batch(buf, offs, lens, all_devices=True), want5)
 
 
+def _lens_shape(kind, n, rng):
+    if kind == "equal":
+        return np.full(n, 1500, np.uint32)
+    if kind == "bimodal":
+        return rng.choice(np.array([0, 4000], np.uint32), n)
+    if kind == "wide":
+        return (rng.random(n) ** 3 * 100_000).astype(np.uint32)           # long tail: scaled buckets
+    if kind == "descending":
+        return np.linspace(3000, 0, n).astype(np.uint32)
+    return rng.integers(1000, 2001, n).astype(np.uint32)                   # the md5var bench shape
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort", [1, 0])
+@pytest.mark.parametrize("n,kind", [(1, "uniform"), (64, "uniform"), (65, "bimodal"), (255, "wide"), (256, "uniform"),
+                                    (257, "descending"), (1000, "equal"), (4097, "bimodal"), (9001, "wide"),
+                                    (65536, "uniform")])
+def test_variable_records_bucketed(brb, orc, torch_dev, n, kind, sort):
+    """Length bucketing of BRB_MD5Batch / BrbSha1_Batch (digest_var_line.h sorted_record): inside
+    every chunk of 256 records the groups are formed by length bucket, and each digest must still
+    land in its record's slot.  Chunk edges (n not a multiple of 64 or 256, a last chunk with fewer
+    groups), equal lengths, two far-apart lengths, a long tail (scaled buckets), descending lengths
+    and the bench's U[1000, 2000]; "var_sort" on and off (caller-order groups) vs the oracle."""
+    rng = np.random.default_rng(n * 7 + len(kind))
+    lens = _lens_shape(kind, n, rng)
+    span = int(lens.astype(np.uint64).sum() + 64 * n + 4096)
+    offs = np.cumsum(rng.integers(0, 64, n).astype(np.uint64) + np.concatenate([[0], lens[:-1]]).astype(np.uint64))
+    offs = offs.astype(np.uint64)
+    buf = workload.gen_records(0x5EED0014, n, 1, span)
+    want5 = orc.md5_batch(buf, offs, lens, threads=16)
+    want1 = orc.sha1_batch(buf, offs, lens, threads=16)
+    d, o, ln = to_dev(torch_dev, buf), to_dev(torch_dev, offs.view(np.int64)), to_dev(torch_dev, lens.view(np.int32))
+    with brb.TestOption("var_sort", sort):
+        assert np.array_equal(brb.md5_batch(d, o, ln).cpu().numpy(), want5)
+        assert np.array_equal(brb.sha1_batch(d, o, ln).cpu().numpy(), want1)
+        assert np.array_equal(brb.md5_batch(buf, offs, lens), want5)
+
+
 @pytest.mark.gpu
 def test_variable_records_wide_span(brb, orc, torch_dev):
     """Groups whose records lie more than 2 GiB apart (32-bit DMA offsets cannot reach them) are

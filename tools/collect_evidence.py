@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Evidence for every kept bench line: the rocprofv3 kernel-trace mean of EXACTLY the dispatches
+inside the line's timed region, and the line's roofline fraction recomputed from it.
+
+tools/gpu_evidence.sh runs each bench line as
+    rocprofv3 --kernel-trace --stats -d <dir>/<line> -o run -- python3 bench.py <args> --mark-timed-region
+bench.py then enqueues one tiny `at::cuda::spin_kernel` right before and one right after each timed
+region (outside its timing), so the dispatches of a region are the ones that start after the first
+sentinel ends and end before the second one starts -- whatever ran before (warm-up, other legs)
+or after (host-mode chunks of the pcie leg, the cfg5 sub-measurement) is excluded by construction.
+(Round 2's collector took "the last K dispatches" of a kernel name, which after the host-mode leg
+were 16 MiB chunks: its cfg4 "timed region" means were not the timed dispatches.)
+
+For each line: per region, the kernels inside it (name, count, mean/min/max duration); the region
+whose dispatch count equals the line's steps x kernels per step is the line's timed region; then
+    frac_rocprof = bytes_per_step / (sum over the step's kernels of their mean duration) / 8 TB/s
+beside the line's own frac (HIP events around the region, which include the ~1-2 us dependent-launch
+gap between back-to-back kernels).  Writes <out>/<line>_timed_region.json, copies the --stats kernel
+summary, and <out>/lines.json with every line + its check (gpu_evidence.sh runs it on the GPU box,
+into gpurun_out/<tag>/evidence; copy that directory to profiles/<tag>_evidence).
+
+Usage: python3 tools/collect_evidence.py gpurun_out/<tag> <out dir>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK = 8000.0
+SENTINEL = "spin_kernel"
+
+
+def dispatches(trace_csv):
+    rows = []
+    with open(trace_csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    return rows
+
+
+def regions(rows):
+    """[(kernel name -> [durations ns]) per region between consecutive sentinel pairs]."""
+    sent = [(s, e) for s, e, n in rows if SENTINEL in n]
+    out = []
+    for i in range(0, len(sent) - 1, 2):
+        lo, hi = sent[i][1], sent[i + 1][0]
+        acc = {}
+        for s, e, n in rows:
+            if s >= lo and e <= hi and SENTINEL not in n:
+                acc.setdefault(n, []).append(e - s)
+        out.append({"span_us": round((hi - lo) / 1e3, 3), "kernels": acc})
+    return out
+
+
+def short(name):
+    return name if len(name) <= 160 else name[:157] + "..."
+
+
+def line_check(line, regs):
+    """Pick the timed region of `line` and recompute its fraction."""
+    r = line.get("roofline") or {}
+    steps = int(line.get("steps", 0))
+    bytes_step = r.get("bytes_per_launch") or r.get("bytes_per_step")
+    event_us = r.get("launch_us_avg") or r.get("step_us_avg")
+    for reg in regs:
+        ks = reg["kernels"]
+        n = sum(len(v) for v in ks.values())
+        if steps and n in (steps, 2 * steps):             # one or two kernels per step
+            per_step_us = sum(sum(v) / len(v) * len(v) / steps for v in ks.values()) / 1e3
+            out = {"timed_dispatches": n, "kernels_per_step": n // steps, "steps": steps,
+                   "kernels": {short(k): {"count": len(v), "mean_us": round(sum(v) / len(v) / 1e3, 3),
+                                          "min_us": round(min(v) / 1e3, 3), "max_us": round(max(v) / 1e3, 3)}
+                               for k, v in ks.items()},
+                   "rocprof_us_per_step": round(per_step_us, 3), "bench_event_us_per_step": event_us,
+                   "region_span_us": reg["span_us"]}
+            if bytes_step:
+                fr = bytes_step / (per_step_us * 1e-6) / 1e9 / PEAK
+                out["bytes_per_step"] = bytes_step
+                out["frac_rocprof"] = round(fr, 4)
+                out["frac_line"] = r.get("frac")
+                if r.get("frac"):
+                    out["frac_line_vs_rocprof"] = round(r["frac"] / fr, 4)
+            return out
+    return None
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    summary = {}
+    for bj in sorted(glob.glob(os.path.join(src, "*.json"))):
+        name = os.path.splitext(os.path.basename(bj))[0]
+        try:
+            line = json.load(open(bj))
+        except (OSError, ValueError):
+            continue
+        traces = glob.glob(os.path.join(src, name, "**", "run_kernel_trace.csv"), recursive=True)
+        stats = glob.glob(os.path.join(src, name, "**", "run_kernel_stats.csv"), recursive=True)
+        entry = {"line": line}
+        if traces:
+            regs = regions(dispatches(traces[0]))
+            chk = line_check(line, regs)
+            entry["timed_region"] = chk
+            if "cfg5" in line:
+                sub = dict(line["cfg5"])
+                sub["roofline"] = {"launch_us_avg": sub.get("launch_us_avg"),
+                                   "bytes_per_launch": sub["records_per_gpu"] * 1500,
+                                   "frac": sub.get("roofline_frac")}
+                entry["cfg5_timed_region"] = line_check(sub, regs)
+            with open(os.path.join(dst, f"{name}_timed_region.json"), "w") as f:
+                json.dump({k: v for k, v in entry.items() if k != "line"}, f, indent=1)
+                f.write("\n")
+        if stats:
+            shutil.copy(stats[0], os.path.join(dst, f"{name}_kernel_stats.csv"))
+        summary[name] = entry
+    with open(os.path.join(dst, "lines.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+        f.write("\n")
+    for name, e in summary.items():
+        t = e.get("timed_region") or {}
+        print(f"{name:12s} frac_line {t.get('frac_line')}  frac_rocprof {t.get('frac_rocprof')}  "
+              f"ratio {t.get('frac_line_vs_rocprof')}  us/step rocprof {t.get('rocprof_us_per_step')} "
+              f"events {t.get('bench_event_us_per_step')}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+// valu_mix.hip -- per-SIMD cost of MIXED VALU instruction streams.
+//
+// valu_tput.hip measured each op class alone: at >= 2 waves per SIMD v_add_u32 / v_xor_b32 /
+// v_bitop3_b32 take ~2 cycles per wave64 instruction, v_alignbit_b32 / v_add3_u32 / v_perm_b32 ~4.
+// The MD5 step mixes them (3 fast + 2 slow), which at 2.8 cycles per instruction would be 30 % faster
+// than the ~4.1 cycles md5_occ.hip measures for the real compression at 1, 2 and 4 waves per SIMD.
+// Here each pattern is 8 independent chains (no dependency stalls), issued by W waves per SIMD;
+// the output is ns and cycles (at the clock measured in-kernel) per wave-instruction per SIMD.
+// Build: hipcc -O3 --offload-arch=gfx950 valu_mix.hip -o valu_mix
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
+#define R4(x) x x x x
+#define R16(x) R4(x) R4(x) R4(x) R4(x)
+
+constexpr int ITERS = 256;
+
+// one group = 8 instructions over 8 registers a..h; z is a shared operand
+#define OPS8(i0, i1, i2, i3, i4, i5, i6, i7) asm volatile(i0 "\n\t" i1 "\n\t" i2 "\n\t" i3 "\n\t" i4 "\n\t" i5 "\n\t" i6 "\n\t" i7 \
+        : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h) : "v"(z))
+
+#define ADD(r) "v_add_u32 %" #r ", %" #r ", %8"
+#define XOR(r) "v_xor_b32 %" #r ", %" #r ", %8"
+#define BOP(r, s) "v_bitop3_b32 %" #r ", %" #r ", %8, %" #s " bitop3:0x96"
+#define ALB(r) "v_alignbit_b32 %" #r ", %" #r ", %" #r ", 7"
+#define ALB2(r, s) "v_alignbit_b32 %" #r ", %" #r ", %" #s ", 7"
+#define AD3(r, s) "v_add3_u32 %" #r ", %" #r ", %8, %" #s
+#define LSL(r) "v_lshlrev_b32 %" #r ", 7, %" #r
+#define LOR(r, s) "v_lshl_or_b32 %" #r ", %" #r ", 7, %" #s
+#define ADDL(r) "v_add_u32 %" #r ", 0x12345678, %" #r
+#define PERM(r) "v_perm_b32 %" #r ", %" #r ", %8, %8"
+
+template <int P>
+__global__ __launch_bounds__(256) void k(unsigned *out, unsigned long long *clk, unsigned seed)
+{
+    unsigned a = seed + threadIdx.x, b = a * 3, c = a ^ 5, d = a + 7, e = a * 11, f = a ^ 13, g = a + 17, h = a * 19;
+    const unsigned z = seed | 1;
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < ITERS; it++) {
+        if constexpr (P == 0) { R16(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADD(4), ADD(5), ADD(6), ADD(7));) }
+        if constexpr (P == 1) { R16(OPS8(ALB(0), ALB(1), ALB(2), ALB(3), ALB(4), ALB(5), ALB(6), ALB(7));) }
+        if constexpr (P == 2) { R16(OPS8(ADD(0), ALB(1), ADD(2), ALB(3), ADD(4), ALB(5), ADD(6), ALB(7));) }
+        if constexpr (P == 3) { R16(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ALB(4), ALB(5), ALB(6), ALB(7));) }
+        if constexpr (P == 4) { R16(OPS8(BOP(0, 1), AD3(1, 2), BOP(2, 3), AD3(3, 4), BOP(4, 5), AD3(5, 6), BOP(6, 7), AD3(7, 0));) }
+        if constexpr (P == 5) { R16(OPS8(ADD(0), ADD(1), ADD(2), ALB(3), ADD(4), ADD(5), ADD(6), ALB(7));) }
+        if constexpr (P == 6) { R16(OPS8(ADD(0), ALB2(1, 0), ADD(2), ALB2(3, 2), ADD(4), ALB2(5, 4), ADD(6), ALB2(7, 6));) }
+        if constexpr (P == 7) { R16(OPS8(XOR(0), ADD(1), XOR(2), ADD(3), XOR(4), ADD(5), XOR(6), ADD(7));) }
+        if constexpr (P == 8) { R16(OPS8(AD3(0, 1), AD3(1, 2), AD3(2, 3), AD3(3, 4), AD3(4, 5), AD3(5, 6), AD3(6, 7), AD3(7, 0));) }
+        if constexpr (P == 9) { R16(OPS8(LSL(0), LSL(1), LSL(2), LSL(3), LSL(4), LSL(5), LSL(6), LSL(7));) }
+        if constexpr (P == 10) { R16(OPS8(LOR(0, 1), LOR(1, 2), LOR(2, 3), LOR(3, 4), LOR(4, 5), LOR(5, 6), LOR(6, 7), LOR(7, 0));) }
+        if constexpr (P == 11) { R16(OPS8(ADDL(0), ADDL(1), ADDL(2), ADDL(3), ADDL(4), ADDL(5), ADDL(6), ADDL(7));) }
+        if constexpr (P == 12) { R16(OPS8(ADD(0), BOP(1, 2), ADD(2), BOP(3, 4), ADD(4), BOP(5, 6), ADD(6), BOP(7, 0));) }
+        if constexpr (P == 13) { R16(OPS8(PERM(0), ADD(1), PERM(2), ADD(3), PERM(4), ADD(5), PERM(6), ADD(7));) }
+        // MD5-like step mix per chain pair: add(literal) bitop3 add3 alignbit add, interleaved over 8 chains
+        if constexpr (P == 14) {
+            R4(OPS8(ADDL(0), ADDL(1), ADDL(2), ADDL(3), BOP(4, 5), BOP(5, 6), BOP(6, 7), BOP(7, 0));
+               OPS8(AD3(0, 4), AD3(1, 5), AD3(2, 6), AD3(3, 7), ALB(4), ALB(5), ALB(6), ALB(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADDL(4), ADDL(5), ADDL(6), ADDL(7));
+               OPS8(BOP(0, 1), BOP(1, 2), BOP(2, 3), BOP(3, 4), AD3(4, 0), AD3(5, 1), AD3(6, 2), AD3(7, 3));
+               OPS8(ALB(0), ALB(1), ALB(2), ALB(3), ADD(4), ADD(5), ADD(6), ADD(7));)
+        }
+        if constexpr (P == 15) { R16(OPS8(ALB(0), ALB(1), ADD(2), ADD(3), ALB(4), ALB(5), ADD(6), ADD(7));) }
+    }
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a + b + c + d + e + f + g + h;
+    if ((threadIdx.x & 63) == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        clk[0] = c1 - c0;
+        clk[1] = r1 - r0;
+    }
+}
+
+constexpr int INSTR_PER_ITER[16] = {128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 160, 128};
+
+template <int P>
+int run(const char *name, int W, int cus)
+{
+    unsigned *o;
+    unsigned long long *clk;
+    CK(hipMalloc(&o, size_t(cus) * W * 256 * 4));
+    CK(hipMalloc(&clk, 16));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int r = 0; r < 4; r++) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k<P>, dim3(cus * W), dim3(256), 0, 0, o, clk, 2u + r);
+        CK(hipEventRecord(e1));
+        CK(hipDeviceSynchronize());
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r)
+            best = std::min(best, ms);
+    }
+    unsigned long long h[2];
+    CK(hipMemcpy(h, clk, 16, hipMemcpyDeviceToHost));
+    const double ghz = double(h[0]) / (double(h[1]) * 10.0);
+    const double instr = double(ITERS) * INSTR_PER_ITER[P] * W;      // per SIMD
+    const double ns = best * 1e6 / instr;
+    printf("%-34s W=%d  %6.3f ns/instr/SIMD  %5.2f cycles @ %.2f GHz\n", name, W, ns, ns * ghz, ghz);
+    hipFree(o);
+    hipFree(clk);
+    return 0;
+}
+
+int main()
+{
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    for (int i = 0; i < 10; i++)
+        run<0>("(warm-up)", 2, cus);
+    for (int W : {1, 2, 4}) {
+        run<0>("add", W, cus);
+        run<11>("add literal", W, cus);
+        run<7>("xor/add alternating", W, cus);
+        run<1>("alignbit", W, cus);
+        run<8>("add3", W, cus);
+        run<9>("lshlrev", W, cus);
+        run<10>("lshl_or", W, cus);
+        run<2>("add/alignbit alternating", W, cus);
+        run<6>("add/alignbit(2 regs) alternating", W, cus);
+        run<3>("4 add then 4 alignbit", W, cus);
+        run<15>("2 alignbit 2 add", W, cus);
+        run<5>("3 add : 1 alignbit", W, cus);
+        run<4>("bitop3/add3 alternating", W, cus);
+        run<12>("add/bitop3 alternating", W, cus);
+        run<13>("perm/add alternating", W, cus);
+        run<14>("MD5 mix (8 chains)", W, cus);
+    }
+    return 0;
+}
