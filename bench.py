@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
+    ap.add_argument("--len-dist", default="uniform", choices=["uniform", "bimodal"],
+                    help="md5var / sha1var record lengths: U[1000, 2000] (default) or a bimodal diagnostic")
     ap.add_argument("--test-option", action="append", default=[], metavar="NAME=VALUE",
                     help="BRB_CryptoGPU_TestOption before the run (A/B of kernel selections)")
     ap.add_argument("--mark-timed-region", action="store_true",
@@ -890,6 +892,8 @@ def bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log):
     n = args.records_per_gpu or 65536
     rng = np.random.default_rng(0x5EED0010 + rank)
     lens_h = rng.integers(1000, 2001, n).astype(np.uint32)
+    if args.len_dist == "bimodal":        # diagnostic: 7 of 8 records 500 B, the others 8 000 B
+        lens_h = np.where(rng.random(n) < 0.125, 8000, 500).astype(np.uint32)
     gaps = rng.integers(0, 16, n).astype(np.uint64)
     offs_h = np.cumsum(gaps + np.concatenate([[0], lens_h[:-1]]).astype(np.uint64)).astype(np.uint64)
     total = int(offs_h[-1] + lens_h[-1])

@@ -17,6 +17,7 @@
 // 65 536 x 1500 bytes.
 #include "brb_kernels.h"
 #include "byte_stream.h"
+#include "test_options.h"
 
 namespace {
 
@@ -85,6 +86,13 @@ BRB_DEV void encode16(const uint16_t *pair, const uint32_t (&a)[16], const uint3
     }
 }
 
+// P pieces per record (lanes P r .. P r + P - 1): encoding has no chain -- every 3 input bytes give
+// their 4 characters on their own -- so a record is cut into P pieces whose lengths are multiples
+// of 3 (all but the last), each encoded by its own lane exactly as a record of its own (only the
+// last piece can end in a partial quantum, and it gets the padding).  65 536 records then fill P
+// waves per SIMD instead of one, whose loads and stores hide each other's latency; adjacent lanes
+// also read adjacent bytes.
+template <int P>
 __global__ __launch_bounds__(kBlock) void b64_encode_kernel(const uint8_t *__restrict__ in,
                                                             const uint64_t *__restrict__ offs,
                                                             const uint32_t *__restrict__ lens, uint64_t n,
@@ -96,15 +104,20 @@ __global__ __launch_bounds__(kBlock) void b64_encode_kernel(const uint8_t *__res
     for (uint32_t e = threadIdx.x; e < 4096; e += kBlock)
         pair[e] = uint16_t(alpha(e >> 6) | (alpha(e & 63) << 8));
     __syncthreads();
-    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t gid = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t r = gid / P;
+    const uint32_t j = uint32_t(gid % P);
     const bool live = r < n;                      // lanes past n only take part in the wave's loads/stores
-    const uint64_t len = live ? lens[r] : 0;
+    const uint64_t rlen = live ? lens[r] : 0;
+    const uint64_t S = 3 * ((rlen + 3 * P - 1) / (3 * P));  // piece bytes, a multiple of 3
+    const uint64_t lo = j * S < rlen ? j * S : rlen;
+    const uint64_t len = (rlen - lo < S ? rlen - lo : S);   // this lane's piece
     const uint64_t olen = 4 * ((len + 2) / 3);
     const uint32_t wv = threadIdx.x >> 6;
     brb_io::StepSrcW<3> src;
     brb_io::SnkW snk;
-    src.init(in + (live ? offs[r] : 0), len, xin + wv * kXch);
-    snk.init(out + (live ? ooffs[r] : 0), olen, xout + wv * kXch);
+    src.init(in + (live ? offs[r] + lo : 0), len, xin + wv * kXch);
+    snk.init(out + (live ? ooffs[r] + 4 * (lo / 3) : 0), olen, xout + wv * kXch);
     // step st: input bytes [192 st, 192 st + 192) -> characters [256 st, 256 st + 256) = output
     // blocks 4 st .. 4 st + 3; the last step of a record holds its 0..191-byte tail
     const uint64_t full = len / 192;
@@ -316,7 +329,14 @@ hipError_t launch_b64_encode(const uint8_t *in, const uint64_t *offs, const uint
 {
     if (n == 0)
         return hipSuccess;
-    b64_encode_kernel<<<grid_for(n), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs);
+    // one lane per record: two pieces per record (two waves per SIMD at 246 VGPRs) measured slower,
+    // 153.8 -> 167.8 us per 65 536 x 1 500 B round trip (interleaved, gpurun_out/r03b64); test
+    // option b64_pieces = 2 keeps them for A/B
+    const bool two = brb_opt::get(brb_opt::kB64Pieces) == 2;
+    if (two)
+        b64_encode_kernel<2><<<unsigned((2 * n + kBlock - 1) / kBlock), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs);
+    else
+        b64_encode_kernel<1><<<grid_for(n), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs);
     return hipGetLastError();
 }
 

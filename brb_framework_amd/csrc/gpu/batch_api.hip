@@ -999,8 +999,9 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
     } known[] = {{"rc4_sector", brb_opt::kRc4Sector, -1, 1},
                  {"var_line", brb_opt::kVarLine, 0, 1},
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
-                 {"var_sort", brb_opt::kVarSort, 0, 1},
-                 {"devices", brb_opt::kDevices, 0, 64}};
+                 {"var_sort", brb_opt::kVarSort, 0, 2},
+                 {"devices", brb_opt::kDevices, 0, 64},
+                 {"b64_pieces", brb_opt::kB64Pieces, 0, 2}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -81,11 +81,16 @@ constexpr uint32_t kSortNB = 8;       // buckets
 
 // Record of lane `lane` in group g (chunk c = g / kSortCG, j = g % kSortCG), or ~0 when that rank
 // holds no record (past n_rec).  `scratch`: this wave's 4 * 64 * kSortCG bytes of LDS.
+// The slice a group takes is rotated by its round t = g / gridDim.x: workgroup b owns groups
+// b + t gridDim.x, all with the same g mod kSortCG (gridDim.x is a multiple of it), so without the
+// rotation one workgroup in kSortCG took every chunk's longest slice in every round and set the
+// kernel time (measured: no gain at all on 524 288 records).  The kSortCG groups of one chunk share
+// t, so the rotation stays a bijection of the chunk's slices.
 BRB_DEV uint64_t sorted_record(uint64_t g, uint32_t lane, const uint32_t *__restrict__ lens, uint64_t n_rec,
                                uint32_t *scratch)
 {
     const uint64_t c0 = (g / kSortCG) * kSortCG * 64;
-    const uint32_t j = uint32_t(g % kSortCG);
+    const uint32_t j = uint32_t((g % kSortCG + g / gridDim.x) % kSortCG);
     uint32_t it[kSortCG];
     bool ok[kSortCG];
     uint32_t lo = 0xFFFFFFFFu, hi = 0;
@@ -151,7 +156,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
                                                                         const uint64_t *__restrict__ offs,
                                                                         const uint32_t *__restrict__ lens,
                                                                         uint32_t rec_len, uint64_t n_rec,
-                                                                        uint8_t *__restrict__ out)
+                                                                        uint8_t *__restrict__ out,
+                                                                        uint64_t brb_first_sorted = 0)
 {
     constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
     constexpr uint32_t OOB = 0x80000000u;                      // a voffset past every descriptor's range
@@ -190,13 +196,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_var_line_kernel(const ui
         uint32_t vq[8];      // DMA voffsets of rows 8q + lane / 8 (line 0 relative to the descriptor)
         uint32_t lq[8];      // lines of those rows' records
     };
-    // Record of this lane in group g: caller order (64 g + lane), or, for SORT groups past the first
-    // round of tickets (g >= first_sorted: whole chunks, since every wave of the grid takes one group
-    // of the first round and 8 x gridDim.x is a multiple of kSortCG), the length-bucketed order of
-    // sorted_record.  The first round stays in caller order so that no wave waits for a ranking
-    // before its first DMA; a later group's ranking is computed while the group before it runs.
-    // ~0: no record (past n_rec).
-    const uint64_t first_sorted = uint64_t(WAVES) * gridDim.x;
+    // Record of this lane in group g: caller order (64 g + lane), or, for SORT groups from
+    // first_sorted on (0, or the end of the first round of tickets, 8 x gridDim.x: whole chunks
+    // either way, gridDim.x being a multiple of kSortCG), the length-bucketed order of
+    // sorted_record.  A group's ranking is computed while the group before it runs (the first
+    // group's before its first DMA).  ~0: no record (past n_rec).
+    const uint64_t first_sorted = brb_first_sorted;
     auto record_of = [&](uint64_t g) -> uint64_t {
         if (SORT && g >= first_sorted && g < n_groups)
             return sorted_record(g, lane, lens, n_rec, sort_scratch + wv * (64 * kSortCG));
@@ -404,11 +409,17 @@ hipError_t launch_var_line(const uint8_t *data, const uint64_t *offs, const uint
     const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
     // bucketing pays only where waves take several groups (with one group per wave the batch's
     // longest record sets the time whatever the grouping): groups past the first round of tickets
-    const bool sort = brb_opt::get(brb_opt::kVarSort) != 0 && groups > uint64_t(g) * W;
+    // (sorted_record's slice rotation needs whole chunks per round: gridDim.x % kSortCG == 0)
+    const bool sort = brb_opt::get(brb_opt::kVarSort) != 0 && groups > uint64_t(g) * W && g % kSortCG == 0;
+    // every group is bucketed, the first round of tickets too (measured on 524 288 records, bimodal
+    // lengths: 698 us unsorted, 438 us with the first round in caller order, 372 us all sorted;
+    // U[1000, 2000]: 200.8 / 200.0 / 197.5 us); test option var_sort = 2 keeps the first round in
+    // caller order (A/B)
+    const uint64_t first = brb_opt::get(brb_opt::kVarSort) == 2 ? uint64_t(g) * W : 0;
     if (sort && out_al)
-        digest_var_line_kernel<Alg, W, true, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
+        digest_var_line_kernel<Alg, W, true, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out, first);
     else if (sort)
-        digest_var_line_kernel<Alg, W, false, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
+        digest_var_line_kernel<Alg, W, false, false, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out, first);
     else if (out_al)
         digest_var_line_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, offs, lens, 0, n_rec, out);
     else

@@ -371,7 +371,10 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * choice / force the per-stream sink / force the whole-sector sink of the RC4 pass), "var_line" 1/0
  * (variable-length digests on the line kernel / on the per-lane kernel), "fixed_var_line" 1/0
  * (unaligned fixed-stride records on the line kernel / record-relative kernel), "var_sort" 1/0
- * (variable-length batches bucketed by block count / in caller order).  Returns 1 and the previous
+ * (variable-length batches bucketed by length / in caller order; 2 keeps the first round of groups in
+ * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k parts,
+ * part g on device g % count), "b64_pieces" 0/1/2 (base64 encode lanes per record: launcher's choice
+ * / forced).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

@@ -52,8 +52,16 @@ def _records(seed, n, max_len):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pieces", [0, 1, 2])
 @pytest.mark.parametrize("seed,n,max_len", [(1, 500, 40), (2, 300, 3000), (3, 20, 100000)])
-def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len):
+def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len, pieces):
+    """pieces: encode lanes per record (test option b64_pieces; 0 = the launcher's choice): with 2,
+    each record is cut into two pieces encoded by two lanes, the first a multiple of 3 bytes."""
+    with brb.TestOption("b64_pieces", pieces):
+        _encode_decode_batch(brb, orc, torch_dev, seed, n, max_len)
+
+
+def _encode_decode_batch(brb, orc, torch_dev, seed, n, max_len):
     data, offs, lens = _records(seed, n, max_len)
     want = [orc.b64_encode(data[int(o):int(o) + int(L)].tobytes()) for o, L in zip(offs, lens)]
     elens = np.array([len(w) for w in want], np.uint32)

@@ -359,14 +359,16 @@ def _lens_shape(kind, n, rng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("sort", [1, 0])
+@pytest.mark.parametrize("sort", [1, 0, 2])
 @pytest.mark.parametrize("n,kind", [(1, "uniform"), (64, "uniform"), (65, "bimodal"), (255, "wide"), (256, "uniform"),
                                     (257, "descending"), (1000, "equal"), (4097, "bimodal"), (9001, "wide"),
-                                    (65536, "uniform")])
+                                    (65536, "uniform"), (140_001, "bimodal"), (300_000, "uniform")])
 def test_variable_records_bucketed(brb, orc, torch_dev, n, kind, sort):
     """Length bucketing of BRB_MD5Batch / BrbSha1_Batch (digest_var_line.h sorted_record): inside
     every chunk of 256 records the groups are formed by length bucket, and each digest must still
-    land in its record's slot.  Chunk edges (n not a multiple of 64 or 256, a last chunk with fewer
+    land in its record's slot.  Bucketing applies past the first round of tickets (more than
+    2 048 groups on 256 CUs), so the two largest shapes exercise it; the others check the caller-order
+    path the same way.  Chunk edges (n not a multiple of 64 or 256, a last chunk with fewer
     groups), equal lengths, two far-apart lengths, a long tail (scaled buckets), descending lengths
     and the bench's U[1000, 2000]; "var_sort" on and off (caller-order groups) vs the oracle."""
     rng = np.random.default_rng(n * 7 + len(kind))
