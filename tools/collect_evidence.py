@@ -19,7 +19,13 @@ gap between back-to-back kernels).  Writes <out>/<line>_timed_region.json, copie
 summary, and <out>/lines.json with every line + its check (gpu_evidence.sh runs it on the GPU box,
 into gpurun_out/<tag>/evidence; copy that directory to profiles/<tag>_evidence).
 
-Usage: python3 tools/collect_evidence.py gpurun_out/<tag> <out dir>
+Under the profiler every dispatch gets ~1.8 us of extra gap (cfg2: 22.74 us per step by the
+events of the profiled run, 20.89 us rocprof kernel mean, 20.99 us by the events of an unprofiled
+run), so the line to compare with the rocprof mean is the UNPROFILED one: with a third argument
+(the directory of tools/gpu_bench_all.sh's unprofiled lines, same names) each entry also carries
+that line's frac and its ratio to frac_rocprof.
+
+Usage: python3 tools/collect_evidence.py gpurun_out/<tag> <out dir> [gpurun_out/<unprofiled tag>]
 """
 import csv
 import glob
@@ -90,6 +96,7 @@ def line_check(line, regs):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
+    plain = sys.argv[3] if len(sys.argv) > 3 else None
     os.makedirs(dst, exist_ok=True)
     summary = {}
     for bj in sorted(glob.glob(os.path.join(src, "*.json"))):
@@ -114,6 +121,21 @@ def main():
             with open(os.path.join(dst, f"{name}_timed_region.json"), "w") as f:
                 json.dump({k: v for k, v in entry.items() if k != "line"}, f, indent=1)
                 f.write("\n")
+        if plain and entry.get("timed_region"):
+            try:
+                pl = json.load(open(os.path.join(plain, name + ".json")))
+            except (OSError, ValueError):
+                pl = None
+            if pl and (pl.get("roofline") or {}).get("frac"):
+                t = entry["timed_region"]
+                t["frac_unprofiled_line"] = pl["roofline"]["frac"]
+                t["unprofiled_event_us_per_step"] = pl["roofline"].get("launch_us_avg", pl["roofline"].get("step_us_avg"))
+                if t.get("frac_rocprof"):
+                    t["frac_unprofiled_vs_rocprof"] = round(pl["roofline"]["frac"] / t["frac_rocprof"], 4)
+                entry["unprofiled_line"] = pl
+            with open(os.path.join(dst, f"{name}_timed_region.json"), "w") as f:
+                json.dump({k: v for k, v in entry.items() if k not in ("line", "unprofiled_line")}, f, indent=1)
+                f.write("\n")
         if stats:
             shutil.copy(stats[0], os.path.join(dst, f"{name}_kernel_stats.csv"))
         summary[name] = entry
@@ -122,9 +144,9 @@ def main():
         f.write("\n")
     for name, e in summary.items():
         t = e.get("timed_region") or {}
-        print(f"{name:12s} frac_line {t.get('frac_line')}  frac_rocprof {t.get('frac_rocprof')}  "
-              f"ratio {t.get('frac_line_vs_rocprof')}  us/step rocprof {t.get('rocprof_us_per_step')} "
-              f"events {t.get('bench_event_us_per_step')}")
+        print(f"{name:9s} rocprof {t.get('rocprof_us_per_step')} us -> frac {t.get('frac_rocprof')} | unprofiled line "
+              f"{t.get('unprofiled_event_us_per_step')} us frac {t.get('frac_unprofiled_line')} "
+              f"(ratio {t.get('frac_unprofiled_vs_rocprof')}) | profiled line frac {t.get('frac_line')}")
 
 
 if __name__ == "__main__":

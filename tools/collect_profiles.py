@@ -31,8 +31,9 @@ def pmc_means(d, pat):
 
 
 def timed_region(trace_csv, pat, bench_json):
-    """Mean duration of the last K dispatches matching `pat` (K = the bench's timed steps; the
-    dispatches before them are the warm-up), next to the bench's own HIP-event launch average."""
+    """SUPERSEDED by tools/collect_evidence.py (round 3): this takes the last K dispatches matching
+    `pat`, which after bench.py's host-mode leg are its 16 MiB chunks, not the timed dispatches
+    (What's weak 4).  Kept only so round-2 tags can be re-derived the way they were."""
     try:
         b = json.load(open(bench_json))
     except (OSError, ValueError):
@@ -117,7 +118,9 @@ def main():
                                ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2),
                                ("pmc_md", "f4_metadata", "metadata_unpack", 1),
                                ("pmc_seg", "f4_md5seg", "md5_seg_kernel", 1),
-                               ("pmc_b64", "f4_base64", "b64_", 2)):
+                               ("pmc_b64", "f4_base64", "b64_", 2),
+                               ("pmc_md5var", "var_md5var", "Md5Alg", 1),
+                               ("pmc_sha1var", "var_sha1var", "Sha1Alg", 1)):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):
             continue

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-benchall}
 mkdir -p "$OUT"
 timeout -k 10 300 python bench.py > "$OUT/cfg2.json" 2> "$OUT/cfg2.err" && echo "cfg2 ok" &&
-timeout -k 10 300 python bench.py --op sha1 --no-cfg5 > "$OUT/cfg2_sha1.json" 2> "$OUT/cfg2_sha1.err" && echo "sha1 ok" &&
+timeout -k 10 300 python bench.py --op sha1 --no-cfg5 > "$OUT/sha1.json" 2> "$OUT/sha1.err" && echo "sha1 ok" &&
 timeout -k 10 300 python bench.py --config 3 > "$OUT/cfg3.json" 2> "$OUT/cfg3.err" && echo "cfg3 ok" &&
 timeout -k 10 300 python bench.py --config 4 > "$OUT/cfg4.json" 2> "$OUT/cfg4.err" && echo "cfg4 ok" &&
 timeout -k 10 300 python bench.py --op rc4 > "$OUT/rc4.json" 2> "$OUT/rc4.err" && echo "rc4 ok" &&
