@@ -1091,8 +1091,10 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                      "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      **traffic_fields(args.pmc_summary, f"f4_{args.op}"),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
-                     "note": "algorithmic bytes read + written per step; one lane per record, so the bound "
-                             "in practice is per-lane issue (MD5 for metadata), DESIGN.md"},
+                     "note": ("algorithmic bytes read + written per step; base64: 32 lanes per record, 12/16-byte "
+                              "pieces, 8 waves per SIMD (HBM-bound, DESIGN.md 4.5)" if args.op == "base64" else
+                              "algorithmic bytes read + written per step; one lane per record, so the bound in "
+                              "practice is per-lane issue (MD5 for metadata), DESIGN.md")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         th = cpu_threads()

@@ -1,4 +1,4 @@
-// base64_kernels.hip -- batched base64 codec, one record per lane.
+// base64_kernels.hip -- batched base64 codec, a group of lanes per record.
 //
 //   encode = brb_base64_encode_to_mb (libbrb_core/crypto/base64.c:304-361): every 3 input bytes
 //            -> 4 characters of the standard alphabet, a 1- or 2-byte tail padded with '='.
@@ -6,15 +6,9 @@
 //            outside the alphabet are skipped, '=' counts as 0 (:363-376), every 4 counted
 //            characters give 3 bytes, a trailing partial group is dropped.
 //
-// A lane streams its record like the RC4 pass (rc4_kernels.hip): 64-byte input blocks with the
-// next one in flight (brb_io::BlockSrc) and 16-byte output stores (brb_io::Snk::put16).  Encode
-// works in steps of 192 input bytes (48 dwords = 16 quanta triples -> 64 output dwords), each 24-bit
-// quantum one v_perm_b32 and two lookups in a 12-bit -> 2-character LDS table.  Decode takes steps
-// of 256 characters while every character is in the alphabet or '=' (then the groups sit at fixed
-// positions: 64 groups -> 192 bytes); at the first step holding a skipped byte or a NUL it falls
-// back to the reference's character-serial rules for the rest of the record.  The per-lane dword
-// reader of the first version (one dword in flight) left both at ~1.2 ms per round trip of
-// 65 536 x 1500 bytes.
+// History (65 536 x 1500 B round trip): one lane per record with a per-lane dword reader, ~1.2 ms;
+// per-lane 64-byte blocks, 235 us (round 2); wave-cooperative 192/256-byte steps through a per-wave
+// LDS exchange, 154 us (round 3, 1 wave per SIMD at 246-497 VGPRs); the group kernels below, 91 us.
 #include "brb_kernels.h"
 #include "byte_stream.h"
 #include "test_options.h"
@@ -22,19 +16,6 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr uint32_t kWaves = kBlock / 64;
-constexpr uint32_t kXch = 4096;                 // per-wave exchange of the cooperative loads / stores
-
-// Wave-uniform maximum (loop bounds of the cooperative loads and stores).
-BRB_DEV uint32_t wave_max(uint32_t x)
-{
-#pragma unroll
-    for (int o = 32; o; o >>= 1) {
-        const uint32_t y = uint32_t(__shfl_xor(int(x), o));
-        x = y > x ? y : x;
-    }
-    return __builtin_amdgcn_readfirstlane(x);
-}
 
 BRB_DEV uint32_t alpha(uint32_t i)   // base64.c:42
 {
@@ -57,99 +38,6 @@ BRB_DEV uint32_t quantum(uint32_t d0, uint32_t d1, uint32_t d2, int q)
 BRB_DEV uint32_t chars4(const uint16_t *pair, uint32_t v)
 {
     return uint32_t(pair[v >> 12]) | (uint32_t(pair[v & 4095u]) << 16);
-}
-
-template <int I>
-BRB_DEV uint32_t pick(const uint32_t (&a)[16], const uint32_t (&b)[16], const uint32_t (&c)[16])
-{
-    return I < 16 ? a[I & 15] : I < 32 ? b[I & 15] : c[I & 15];
-}
-
-// the 16 output dwords of triples 4h .. 4h + 3 of a 48-dword step
-template <int H>
-BRB_DEV void encode16(const uint16_t *pair, const uint32_t (&a)[16], const uint32_t (&b)[16], const uint32_t (&c)[16],
-                      uint32_t (&o)[16])
-{
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-        const int t = 4 * H + g;
-        uint32_t d0, d1, d2;
-        switch (t) {   // compile-time register indices
-#define BRB_T(T) case T: d0 = pick<3 * T>(a, b, c); d1 = pick<3 * T + 1>(a, b, c); d2 = pick<3 * T + 2>(a, b, c); break;
-            BRB_T(0) BRB_T(1) BRB_T(2) BRB_T(3) BRB_T(4) BRB_T(5) BRB_T(6) BRB_T(7)
-            BRB_T(8) BRB_T(9) BRB_T(10) BRB_T(11) BRB_T(12) BRB_T(13) BRB_T(14) default: BRB_T(15)
-#undef BRB_T
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            o[4 * g + q] = chars4(pair, quantum(d0, d1, d2, q));
-    }
-}
-
-// P pieces per record (lanes P r .. P r + P - 1): encoding has no chain -- every 3 input bytes give
-// their 4 characters on their own -- so a record is cut into P pieces whose lengths are multiples
-// of 3 (all but the last), each encoded by its own lane exactly as a record of its own (only the
-// last piece can end in a partial quantum, and it gets the padding).  65 536 records then fill P
-// waves per SIMD instead of one, whose loads and stores hide each other's latency; adjacent lanes
-// also read adjacent bytes.
-template <int P>
-__global__ __launch_bounds__(kBlock) void b64_encode_kernel(const uint8_t *__restrict__ in,
-                                                            const uint64_t *__restrict__ offs,
-                                                            const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint8_t *__restrict__ out,
-                                                            const uint64_t *__restrict__ ooffs)
-{
-    __shared__ uint16_t pair[4096];
-    __shared__ __attribute__((aligned(16))) uint8_t xin[kWaves * kXch], xout[kWaves * kXch];
-    for (uint32_t e = threadIdx.x; e < 4096; e += kBlock)
-        pair[e] = uint16_t(alpha(e >> 6) | (alpha(e & 63) << 8));
-    __syncthreads();
-    const uint64_t gid = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    const uint64_t r = gid / P;
-    const uint32_t j = uint32_t(gid % P);
-    const bool live = r < n;                      // lanes past n only take part in the wave's loads/stores
-    const uint64_t rlen = live ? lens[r] : 0;
-    const uint64_t S = 3 * ((rlen + 3 * P - 1) / (3 * P));  // piece bytes, a multiple of 3
-    const uint64_t lo = j * S < rlen ? j * S : rlen;
-    const uint64_t len = (rlen - lo < S ? rlen - lo : S);   // this lane's piece
-    const uint64_t olen = 4 * ((len + 2) / 3);
-    const uint32_t wv = threadIdx.x >> 6;
-    brb_io::StepSrcW<3> src;
-    brb_io::SnkW snk;
-    src.init(in + (live ? offs[r] + lo : 0), len, xin + wv * kXch);
-    snk.init(out + (live ? ooffs[r] + 4 * (lo / 3) : 0), olen, xout + wv * kXch);
-    // step st: input bytes [192 st, 192 st + 192) -> characters [256 st, 256 st + 256) = output
-    // blocks 4 st .. 4 st + 3; the last step of a record holds its 0..191-byte tail
-    const uint64_t full = len / 192;
-    const uint32_t t = uint32_t(len - 192 * full);            // 0..191 tail bytes (zeros past them)
-    const uint32_t qfull = t / 3, rest = t % 3;               // quantum qfull holds the 1- or 2-byte tail
-    const uint32_t nloop = wave_max(uint32_t(full + (t ? 1 : 0)));
-    uint32_t blk[3][16], o[4][16];
-    if (nloop) {
-        src.issue(0);
-        src.take(blk);
-    }
-    for (uint32_t st = 0; st < nloop; st++) {
-        if (st + 1 < nloop)
-            src.issue(st + 1);                                // in flight while step st is encoded
-        const bool in_full = st < full, in_tail = st == full && t;
-        // the padding rule of base64.c:335-352 (bytes past the record read as 0 above)
-        auto pad = [&](uint32_t v, uint32_t u) {
-            return in_tail && u == qfull && rest ? (rest == 1 ? (v & 0x0000FFFFu) | 0x3D3D0000u : (v & 0x00FFFFFFu) | 0x3D000000u) : v;
-        };
-#define BRB_ENC(H)                                                                          \
-        encode16<H>(pair, blk[0], blk[1], blk[2], o[H]);                                    \
-        _Pragma("unroll") for (int k = 0; k < 16; k++) o[H][k] = pad(o[H][k], 16 * H + k);
-        BRB_ENC(0) BRB_ENC(1) BRB_ENC(2) BRB_ENC(3)
-#undef BRB_ENC
-        if (st + 1 < nloop)
-            src.take(blk);                                    // before this step's stores (StepSrcW)
-#pragma unroll
-        for (int h = 0; h < 4; h++)
-            snk.put16(o[h], 4 * st + h, in_full || (in_tail && t > 48u * h));
-    }
-    if (live)
-        snk.flush();                                          // Snk writes no byte past olen
 }
 
 // base64.c:363-376: alphabet value, 0 for '=', -1 for anything else (NUL included)
@@ -178,111 +66,182 @@ BRB_DEV uint32_t group3(const int8_t *val, uint32_t ch)
     return s | (uint32_t(v0 | v1 | v2 | v3) & 0x80000000u);
 }
 
-// 16 groups (one 64-character block) -> 12 output dwords at o[12 k ..]; flag word q (bit 31 set: a
-// character outside the alphabet / '=') covers groups 4q .. 4q + 3, one bit 31 per group in
-// bits 31, 30, 29, 28 so that a partial step can ignore the groups past its end (group_mask)
-BRB_DEV void decode_block4(const int8_t *val, const uint32_t (&c)[16], uint32_t (&o)[48], int k, uint32_t (&f)[4])
-{
-#pragma unroll
-    for (int g = 0; g < 16; g += 4) {
-        const uint32_t s0 = group3(val, c[g]), s1 = group3(val, c[g + 1]), s2 = group3(val, c[g + 2]),
-                       s3 = group3(val, c[g + 3]);
-        f[g / 4] = (s0 & 0x80000000u) | ((s1 >> 1) & 0x40000000u) | ((s2 >> 2) & 0x20000000u) | ((s3 >> 3) & 0x10000000u);
-        const int q = 12 * k + 3 * (g / 4);
-        o[q] = (s0 & 0xFFFFFFu) | (s1 << 24);
-        o[q + 1] = ((s1 & 0xFFFFFFu) >> 8) | (s2 << 16);
-        o[q + 2] = ((s2 & 0xFFFFFFu) >> 16) | (s3 << 8);
-    }
-}
+// ---- group kernels: G lanes per record, 12 / 16-byte pieces -------------------------------------
+//
+// Neither direction of the codec carries state along a record (every 3 bytes <-> 4 characters on
+// their own, while the characters are clean), so a record is cut into pieces: encode 12 input bytes
+// -> 16 characters, decode 16 characters -> 12 bytes.  G lanes (a power of two, 1..64) work on one
+// record, lane j of the group on pieces j, j + G, ...; a piece is one 16/12-byte access at a lane
+// stride of 12/16 bytes, so a group's loads and stores are contiguous runs of 12 G / 16 G bytes,
+// and the kernels hold 46 (encode) / 64 (decode) VGPRs -- 8 waves per SIMD instead of the
+// lane-per-record kernels' 1 to 2, which waited on memory 36 % of the time.  The grid is persistent
+// (kPersist workgroups): group k walks records k, k + groups, ...
 
-// flags of the first m (>= 1) groups of a flag word, folded onto bit 31
-BRB_DEV uint32_t group_mask(uint32_t m)
-{
-    return m >= 4 ? 0xF0000000u : (0xF0000000u << (4 - m)) & 0xF0000000u;
-}
+constexpr unsigned kPersist = 2048;              // 8 workgroups of 4 waves on each of 256 CUs
 
-__global__ __launch_bounds__(kBlock) void b64_decode_kernel(const uint8_t *__restrict__ in,
-                                                            const uint64_t *__restrict__ offs,
-                                                            const uint32_t *__restrict__ lens, uint64_t n,
-                                                            uint8_t *__restrict__ out,
-                                                            const uint64_t *__restrict__ ooffs,
-                                                            uint32_t *__restrict__ olens)
+// bytes [a, a + m) (m <= 16) as 4 little-endian dwords, zeros past m.  Reads only dwords that hold
+// a byte of the range (so never past the end of a buffer); one 16-byte load when aligned and whole.
+BRB_DEV void load_piece(const uint8_t *a, uint32_t m, uint32_t (&d)[4])
 {
-    __shared__ int8_t val[256];
-    __shared__ __attribute__((aligned(16))) uint8_t xin[kWaves * kXch], xout[kWaves * kXch];
-    for (uint32_t e = threadIdx.x; e < 256; e += kBlock)
-        val[e] = int8_t(b64_value(e));
-    __syncthreads();
-    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    const bool live = r < n;                      // lanes past n only take part in the wave's loads/stores
-    const uint64_t len = live ? lens[r] : 0;
-    const uint8_t *a = in + (live ? offs[r] : 0);
-    const uint32_t wv = threadIdx.x >> 6;
-    brb_io::SnkW snk;
-    snk.init(out + (live ? ooffs[r] : 0), 3 * (len / 4), xout + wv * kXch);
-    // Steps of 256 characters (4 input blocks -> 64 groups -> 3 output blocks) in one wave-uniform
-    // loop.  A lane's last step may be partial: its whole groups decode the same way and a trailing
-    // partial group is dropped (base64.c:171-175).  At the first step whose whole groups hold a byte
-    // outside the alphabet / '=' (a skipped byte or a NUL), the lane leaves the loop's output and
-    // finishes with the reference's character-serial rules from that step's start.
-    uint64_t pos = 0;
-    uint32_t produced = 0;
-    bool fast = true;
-    {
-        brb_io::StepSrcW<4> src;
-        src.init(a, len, xin + wv * kXch);
-        const uint32_t nloop = wave_max(uint32_t((len + 255) / 256));
-        uint32_t c[4][16], o[48];
-        if (nloop) {
-            src.issue(0);
-            src.take(c);
-        }
-        for (uint32_t st = 0; st < nloop; st++) {
-            if (st + 1 < nloop)
-                src.issue(st + 1);
-            const uint64_t p0 = 256ull * st;
-            const uint32_t nch = fast && p0 < len ? uint32_t(len - p0 < 256 ? len - p0 : 256) : 0u;
-            const uint32_t ng = nch / 4;                          // whole groups of this step
-            uint32_t bad = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                uint32_t b4[4];
-                decode_block4(val, c[k], o, k, b4);
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    bad |= 16u * k + 4u * q < ng ? b4[q] & group_mask(ng - 16u * k - 4u * q) : 0u;
-            }
-            const bool act = nch && !bad;
-            if (nch && !act) {
-                fast = false;                                     // serial from this step's start
-                pos = p0;
-            }
-            if (act) {
-                pos = p0 + nch;
-                produced += 3 * ng;
-            }
-            if (st + 1 < nloop)
-                src.take(c);
-#pragma unroll
-            for (int q = 0; q < 3; q++) {
-                uint32_t h[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++)
-                    h[i] = o[16 * q + i];
-                snk.put16(h, 3 * st + q, act && 3 * ng > 64u * q);
-            }
-        }
-    }
-    if (!live)
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(a);
+    const uint32_t s = uint32_t(ad & 3);
+    if (s == 0 && m == 16) {
+        const uint4 v = ld16_a4(a);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
         return;
-    // base64.c:131-179, character by character, from pos (a group boundary: val = cnt = 0); after
-    // the fast loop only a lane that met a skipped byte or a NUL, or a trailing partial group, is left
-    brb_io::Snk &ss = snk.s;
+    }
+    const uint8_t *a0 = a - s;
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        w[k] = m && 4u * k < s + m ? ld4_a4(a0 + 4 * k) : 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t v = funnel(w[k + 1], w[k], 8 * s);
+        const uint32_t lo = 4u * k;
+        d[k] = m >= lo + 4 ? v : m > lo ? v & (0xFFFFFFFFu >> (32 - 8 * (m - lo))) : 0u;
+    }
+}
+
+// 12 bytes [a, a + 12), 4-byte aligned: three dword loads the compiler merges into one dwordx3
+BRB_DEV void load12_a4(const uint8_t *a, uint32_t (&d)[4])
+{
+    d[0] = ld4_a4(a);
+    d[1] = ld4_a4(a + 4);
+    d[2] = ld4_a4(a + 8);
+    d[3] = 0;
+}
+
+// the q (<= 16) bytes of v -> [o, o + q), writing no byte outside it: aligned dwords that the range
+// covers whole go out as dword (or one 16-byte) stores, the partial dwords at its ends byte by byte
+BRB_DEV void store_piece(uint8_t *o, uint32_t q, const uint32_t (&v)[4])
+{
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(o);
+    const uint32_t s = uint32_t(ad & 3);
+    if (s == 0 && q == 16) {
+        st16_a4(o, v[0], v[1], v[2], v[3]);
+        return;
+    }
+    if (s == 0 && q == 12) {
+        stg(reinterpret_cast<uint32_t *>(o), v[0]);
+        stg(reinterpret_cast<uint32_t *>(o + 4), v[1]);
+        stg(reinterpret_cast<uint32_t *>(o + 8), v[2]);
+        return;
+    }
+    uint8_t *a0 = o - s;
+    // aligned dword k holds range bytes 4k - s .. 4k - s + 3: byte b = byte 4 + b - s of {v_k : v_k-1}
+    const uint32_t sel = 0x07060504u - 0x01010101u * s;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        const uint32_t first = 4u * k;                       // position of the dword in [a0, ...)
+        if (first >= s + q)
+            break;
+        const uint32_t w = __builtin_amdgcn_perm(k < 4 ? v[k] : 0u, k > 0 ? v[k - 1] : 0u, sel);
+        const uint32_t lo = first < s ? s - first : 0u;      // 0, or s in dword 0
+        const uint32_t end = s + q - first;                  // bytes of this dword before the end
+        const uint32_t hi = end >= 4 ? 3u : end - 1;
+        if (lo == 0 && hi == 3) {
+            stg(reinterpret_cast<uint32_t *>(a0 + first), w);
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < 4; b++)
+                if (b >= lo && b <= hi)
+                    stg8(a0 + first + b, w >> (8 * b));
+        }
+    }
+}
+
+// one encode piece: m (1..12) input bytes in d[0..2] (zeros past m) -> 4 * ceil(m / 3) characters
+BRB_DEV uint32_t encode_piece(const uint16_t *pair, const uint32_t (&d)[4], uint32_t m, uint32_t (&c)[4])
+{
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        c[q] = chars4(pair, quantum(d[0], d[1], d[2], q));
+    if (m < 12) {                                             // the record's last piece
+        const uint32_t nq = (m + 2) / 3, rest = m % 3;        // base64.c:335-352 padding
+        if (rest) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (uint32_t(q) == nq - 1)
+                    c[q] = rest == 1 ? (c[q] & 0x0000FFFFu) | 0x3D3D0000u : (c[q] & 0x00FFFFFFu) | 0x3D000000u;
+        }
+        return 4 * nq;
+    }
+    return 16;
+}
+
+__global__ __launch_bounds__(kBlock) void b64_encode_group_kernel(const uint8_t *__restrict__ in,
+                                                                  const uint64_t *__restrict__ offs,
+                                                                  const uint32_t *__restrict__ lens, uint64_t n,
+                                                                  uint8_t *__restrict__ out,
+                                                                  const uint64_t *__restrict__ ooffs, uint32_t lg)
+{
+    __shared__ uint16_t pair[4096];
+    for (uint32_t e = threadIdx.x; e < 4096; e += kBlock)
+        pair[e] = uint16_t(alpha(e >> 6) | (alpha(e & 63) << 8));
+    __syncthreads();
+    const uint32_t G = 1u << lg, sub = threadIdx.x & (G - 1);
+    const uint64_t groups = uint64_t(gridDim.x) * (kBlock >> lg);
+    for (uint64_t r = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) >> lg; r < n; r += groups) {
+        const uint64_t len = lens[r];
+        const uint8_t *a = in + offs[r];
+        uint8_t *o = out + ooffs[r];
+        const uint64_t np = (len + 11) / 12;
+        const bool al = (reinterpret_cast<uintptr_t>(a) & 3) == 0;
+        // two pieces per lane per pass (p, p + G): both loads in flight before either is encoded (four
+        // measured slower: 88 VGPRs, 5 waves per SIMD)
+        for (uint64_t p = sub; p < np; p += 2 * G) {
+            uint32_t d[2][4], m[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint64_t pu = p + u * G;
+                m[u] = pu < np ? (len - 12 * pu >= 12 ? 12u : uint32_t(len - 12 * pu)) : 0u;
+                if (al && m[u] == 12)
+                    load12_a4(a + 12 * pu, d[u]);
+                else
+                    load_piece(a + 12 * pu, m[u], d[u]);      // m == 0: nothing is read
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (m[u]) {
+                    uint32_t c[4];
+                    const uint32_t q = encode_piece(pair, d[u], m[u], c);
+                    store_piece(o + 16 * (p + u * G), q, c);
+                }
+            }
+        }
+    }
+}
+
+// one decode piece: the 16 characters in d; returns the flags of its first `groups` groups (bit 31
+// set: a character outside the alphabet / '=' among them) and the 12 bytes in b[0..2]
+BRB_DEV uint32_t decode_piece(const int8_t *val, const uint32_t (&d)[4], uint32_t groups, uint32_t (&b)[4])
+{
+    const uint32_t s0 = group3(val, d[0]), s1 = group3(val, d[1]), s2 = group3(val, d[2]), s3 = group3(val, d[3]);
+    b[0] = (s0 & 0xFFFFFFu) | (s1 << 24);
+    b[1] = ((s1 & 0xFFFFFFu) >> 8) | (s2 << 16);
+    b[2] = ((s2 & 0xFFFFFFu) >> 16) | (s3 << 8);
+    b[3] = 0;
+    const uint32_t f = (s0 & (groups > 0 ? 0x80000000u : 0u)) | (s1 & (groups > 1 ? 0x80000000u : 0u)) |
+                       (s2 & (groups > 2 ? 0x80000000u : 0u)) | (s3 & (groups > 3 ? 0x80000000u : 0u));
+    return f;
+}
+
+// base64.c:131-179 character by character from character `pos` of a record (a group boundary,
+// val = cnt = 0 there) with `produced` bytes already written; returns the record's output length
+BRB_DEV uint32_t decode_serial(const int8_t *val, const uint8_t *a, uint64_t len, uint64_t pos, uint8_t *o,
+                               uint32_t produced)
+{
+    brb_io::Snk ss;
+    ss.init(o + produced, 3 * (len / 4) - produced);
     brb_io::Src src;
     src.init(a + pos, len - pos);
     uint32_t val4 = 0, cnt = 0, outn = 0;
     uint64_t outacc = 0;
-    bool on = !fast;
+    bool on = true;
     for (uint64_t c4 = pos; c4 < len && on; c4 += 4) {
         const uint32_t chunk = src.next();
         const uint32_t nb = len - c4 >= 4 ? 4u : uint32_t(len - c4);
@@ -315,37 +274,104 @@ __global__ __launch_bounds__(kBlock) void b64_decode_kernel(const uint8_t *__res
         ss.put(uint32_t(outacc));
     }
     ss.flush();
-    olens[r] = produced;
+    return produced;
 }
 
-inline unsigned grid_for(uint64_t n) { return unsigned((n + kBlock - 1) / kBlock); }
+// Pieces before a record's first piece with a character outside the alphabet / '=' in its whole
+// groups decode at fixed positions; from that piece's start the group's first lane finishes the
+// record with the reference's serial rules (a skipped byte shifts every later group; a NUL ends
+// the string).  The group finds that piece with one ballot per half pass, so no lane stores a
+// piece at or after it.  Characters of a trailing partial group never produce output.
+__global__ __launch_bounds__(kBlock) void b64_decode_group_kernel(const uint8_t *__restrict__ in,
+                                                                  const uint64_t *__restrict__ offs,
+                                                                  const uint32_t *__restrict__ lens, uint64_t n,
+                                                                  uint8_t *__restrict__ out,
+                                                                  const uint64_t *__restrict__ ooffs,
+                                                                  uint32_t *__restrict__ olens, uint32_t lg)
+{
+    __shared__ int8_t val[256];
+    for (uint32_t e = threadIdx.x; e < 256; e += kBlock)
+        val[e] = int8_t(b64_value(e));
+    __syncthreads();
+    const uint32_t G = 1u << lg, lane = threadIdx.x & 63, sub = lane & (G - 1), gbase = lane - sub;
+    const uint64_t gmask = G == 64 ? ~0ull : ((1ull << G) - 1) << gbase;
+    const uint64_t groups = uint64_t(gridDim.x) * (kBlock >> lg);
+    for (uint64_t r = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) >> lg; r < n; r += groups) {
+        const uint64_t len = lens[r];
+        const uint8_t *a = in + offs[r];
+        uint8_t *o = out + ooffs[r];
+        const uint64_t ng = len / 4;                          // whole groups
+        const uint64_t np = (ng + 3) / 4;                     // pieces holding a whole group
+        uint64_t dirty = ~0ull;                               // first piece with a skipped byte / NUL
+        for (uint64_t p = sub; p < np; p += 2 * G) {         // pieces p and p + G: both loads in flight
+            const uint64_t p1 = p + G;
+            const uint32_t g0 = ng - 4 * p >= 4 ? 4u : uint32_t(ng - 4 * p);
+            const uint32_t g1 = p1 < np ? (ng - 4 * p1 >= 4 ? 4u : uint32_t(ng - 4 * p1)) : 0u;
+            uint32_t d0[4], d1[4], b0[4], b1[4];
+            load_piece(a + 16 * p, 4 * g0, d0);
+            load_piece(a + 16 * p1, 4 * g1, d1);              // g1 == 0: nothing is read
+            const uint32_t f0 = decode_piece(val, d0, g0, b0), f1 = decode_piece(val, d1, g1, b1);
+            const uint64_t m0 = (__builtin_amdgcn_ballot_w64(f0 != 0) & gmask) >> gbase;
+            const uint64_t m1 = (__builtin_amdgcn_ballot_w64(f1 != 0) & gmask) >> gbase;
+            const uint64_t base = p - sub;
+            if (m0 | m1)
+                dirty = m0 ? base + __builtin_ctzll(m0) : base + G + __builtin_ctzll(m1);
+            if (p < dirty)
+                store_piece(o + 12 * p, 3 * g0, b0);
+            if (g1 && p1 < dirty)
+                store_piece(o + 12 * p1, 3 * g1, b1);
+            if (dirty != ~0ull)
+                break;                                        // group-uniform
+        }
+        if (sub == 0)
+            olens[r] = dirty == ~0ull ? uint32_t(3 * ng) : decode_serial(val, a, len, 16 * dirty, o, uint32_t(12 * dirty));
+    }
+}
+
+// log2 of the lanes per record: an average record takes two passes of two pieces per lane, at most
+// 32 lanes (measured on 65 536 x 1500 B: 16 / 32 / 64 lanes 96.0 / 90.7 / 92.2 us per round trip);
+// mean_len 0 = unknown (device mode): 32 lanes.  The test option forces it.
+uint32_t group_lg(uint64_t mean_len, uint32_t piece)
+{
+    const int forced = brb_opt::get(brb_opt::kB64Group);
+    if (forced >= 0 && forced <= 6)
+        return uint32_t(forced);
+    if (mean_len == 0)
+        return 5;
+    const uint64_t quarter = (mean_len + 4 * piece - 1) / (4 * piece);
+    uint32_t lg = 0;
+    while (lg < 5 && (1ull << lg) < quarter)
+        lg++;
+    return lg;
+}
+
+unsigned group_grid(uint64_t n, uint32_t lg)
+{
+    const uint64_t blocks = ((n << lg) + kBlock - 1) / kBlock;
+    return unsigned(blocks < kPersist ? blocks : kPersist);
+}
 
 }  // namespace
 
 namespace brb {
 
 hipError_t launch_b64_encode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
-                             const uint64_t *ooffs, hipStream_t s)
+                             const uint64_t *ooffs, uint64_t mean_len, hipStream_t s)
 {
     if (n == 0)
         return hipSuccess;
-    // one lane per record: two pieces per record (two waves per SIMD at 246 VGPRs) measured slower,
-    // 153.8 -> 167.8 us per 65 536 x 1 500 B round trip (interleaved, gpurun_out/r03b64); test
-    // option b64_pieces = 2 keeps them for A/B
-    const bool two = brb_opt::get(brb_opt::kB64Pieces) == 2;
-    if (two)
-        b64_encode_kernel<2><<<unsigned((2 * n + kBlock - 1) / kBlock), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs);
-    else
-        b64_encode_kernel<1><<<grid_for(n), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs);
+    const uint32_t lg = group_lg(mean_len, 12);
+    b64_encode_group_kernel<<<group_grid(n, lg), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs, lg);
     return hipGetLastError();
 }
 
 hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
-                             const uint64_t *ooffs, uint32_t *olens, hipStream_t s)
+                             const uint64_t *ooffs, uint32_t *olens, uint64_t mean_len, hipStream_t s)
 {
     if (n == 0)
         return hipSuccess;
-    b64_decode_kernel<<<grid_for(n), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs, olens);
+    const uint32_t lg = group_lg(mean_len, 16);
+    b64_decode_group_kernel<<<group_grid(n, lg), kBlock, 0, s>>>(in, offs, lens, n, out, ooffs, olens, lg);
     return hipGetLastError();
 }
 

@@ -725,9 +725,17 @@ int b64_batch(bool decode, const void *in, const uint64_t *offs, const uint32_t 
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipError_t e;
+    uint64_t mean_len = 0;                      // unknown in device mode (the lengths are device memory)
+    if (!(flags & BRB_BATCH_DEVICE)) {
+        uint64_t sum = 0;
+        for (uint64_t i = 0; i < n; i++)
+            sum += lens[i];
+        mean_len = sum / n + 1;
+    }
     auto launch = [&](const uint8_t *i, const uint64_t *o, const uint32_t *l, uint8_t *d, const uint64_t *oo,
                       uint32_t *ol) {
-        return decode ? brb::launch_b64_decode(i, o, l, n, d, oo, ol, s) : brb::launch_b64_encode(i, o, l, n, d, oo, s);
+        return decode ? brb::launch_b64_decode(i, o, l, n, d, oo, ol, mean_len, s)
+                      : brb::launch_b64_encode(i, o, l, n, d, oo, mean_len, s);
     };
     if (flags & BRB_BATCH_DEVICE) {
         if ((e = launch(static_cast<const uint8_t *>(in), offs, lens, static_cast<uint8_t *>(out), ooffs, olens)) != hipSuccess)
@@ -1001,7 +1009,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
                  {"var_sort", brb_opt::kVarSort, 0, 2},
                  {"devices", brb_opt::kDevices, 0, 64},
-                 {"b64_pieces", brb_opt::kB64Pieces, 0, 2}};
+                 {"b64_group", brb_opt::kB64Group, -1, 6}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -31,9 +31,9 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
 
 // base64 (base64_kernels.hip)
 hipError_t launch_b64_encode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
-                             const uint64_t *ooffs, hipStream_t s);
+                             const uint64_t *ooffs, uint64_t mean_len, hipStream_t s);
 hipError_t launch_b64_decode(const uint8_t *in, const uint64_t *offs, const uint32_t *lens, uint64_t n, uint8_t *out,
-                             const uint64_t *ooffs, uint32_t *olens, hipStream_t s);
+                             const uint64_t *ooffs, uint32_t *olens, uint64_t mean_len, hipStream_t s);
 
 // RC4 (rc4_kernels.hip): 264-byte BRB_RC4_State records, updated in place.  Stream i uses
 // states[sidx ? sidx[i] : i] (sidx: a connection table, the transform batcher's indirection).

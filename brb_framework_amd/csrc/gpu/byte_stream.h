@@ -417,185 +417,6 @@ struct BlockSrcW {
     }
 };
 
-// BlockSrcW with NB blocks per step, issue and take split: issue(st) starts the loads of blocks
-// NB st .. NB st + NB - 1, take(c) waits for them and hands them out.  A consumer issues step st + 1,
-// works on step st, takes step st + 1 and only THEN issues step st's stores: on gfx9 one in-order
-// counter (vmcnt) covers loads and stores, and hipcc waits vmcnt(0) before the first use of a
-// loaded register, so loads still in flight behind stores make every wait include the stores
-// (base64 encode: 87.5 us with the stores before the wait, 59 us with no stores at all).  Same loads
-// as BlockSrcW (four lanes per block, 16 blocks per instruction) and the same per-wave exchange,
-// reused block by block.  Every lane calls init(), issue() and take() in uniform control flow; a
-// lane receives zero blocks past its range's end.
-template <int NB>
-struct StepSrcW {
-    const uint32_t *p;
-    uint32_t sh;
-    uint64_t len, ndw;
-    uint64_t nb;         // first block returned by the next take()
-    uint32_t prev;
-    uint8_t *xw;
-    uint32_t lane;
-    uint64_t qa[4];
-    uint64_t qrem[4];
-    uint4 v[NB][4];
-
-    BRB_DEV void issue(uint64_t st)
-    {
-        // the common step: every chunk this lane loads lies inside its range -- NB x 4 plain loads
-        // behind one branch (per-chunk branches cost ~8 instructions per load, AGPR address reads
-        // included, in the base64 kernels)
-        const uint64_t last = 16 * (NB * st + NB - 1) + 4;
-        if (last <= qrem[0] && last <= qrem[1] && last <= qrem[2] && last <= qrem[3]) {
-#pragma unroll
-            for (int j = 0; j < NB; j++)
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 64 * (NB * st + j)));
-        } else {
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const uint64_t base = 16 * (NB * st + j);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    if (base + 4 <= qrem[q]) {
-                        v[j][q] = ld16_a4(reinterpret_cast<const uint8_t *>(qa[q] + 4 * base));
-                    } else {
-                        const uint32_t *d = reinterpret_cast<const uint32_t *>(qa[q]) + base;
-                        v[j][q].x = base + 0 < qrem[q] ? ldg(d + 0) : 0u;
-                        v[j][q].y = base + 1 < qrem[q] ? ldg(d + 1) : 0u;
-                        v[j][q].z = base + 2 < qrem[q] ? ldg(d + 2) : 0u;
-                        v[j][q].w = base + 3 < qrem[q] ? ldg(d + 3) : 0u;
-                    }
-                }
-            }
-        }
-    }
-
-    BRB_DEV void init(const uint8_t *a, uint64_t n, uint8_t *exchange)
-    {
-        const uintptr_t ad = reinterpret_cast<uintptr_t>(a);
-        p = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
-        sh = uint32_t(ad & 3) * 8;
-        len = n;
-        ndw = n ? ((ad & 3) + n + 3) / 4 : 0;
-        prev = ndw ? ldg(p) : 0u;
-        nb = 0;
-        xw = exchange;
-        lane = threadIdx.x & 63;
-        const uint64_t pa = reinterpret_cast<uint64_t>(p);
-        const uint32_t c = lane & 3;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int src = 16 * q + int(lane >> 2);
-            const uint64_t a_r = (uint64_t(uint32_t(__shfl(int(pa >> 32), src))) << 32) | uint32_t(__shfl(int(uint32_t(pa)), src));
-            const uint64_t n_r = (uint64_t(uint32_t(__shfl(int(ndw >> 32), src))) << 32) | uint32_t(__shfl(int(uint32_t(ndw)), src));
-            qa[q] = a_r + 4 * (1 + 4 * c);
-            qrem[q] = n_r > 1 + 4 * c ? n_r - 1 - 4 * c : 0;
-        }
-    }
-
-    BRB_DEV void take(uint32_t (&c)[NB][16])
-    {
-#pragma unroll
-        for (int j = 0; j < NB; j++) {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                *reinterpret_cast<uint4 *>(xw + BlockSrcW::xoff(16 * q + (lane >> 2), lane & 3)) = v[j][q];
-            uint32_t L[16];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint4 t = *reinterpret_cast<const uint4 *>(xw + BlockSrcW::xoff(lane, k));
-                L[4 * k] = t.x;
-                L[4 * k + 1] = t.y;
-                L[4 * k + 2] = t.z;
-                L[4 * k + 3] = t.w;
-            }
-#pragma unroll
-            for (int i = 0; i < 16; i++)
-                c[j][i] = __builtin_amdgcn_alignbit(L[i], i ? L[i - 1] : prev, sh);
-            prev = L[15];
-            const uint64_t pos = 64 * (nb + j);
-            if (pos + 64 > len) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint64_t q = pos + 4 * i;
-                    c[j][i] = q >= len ? 0u : q + 4 <= len ? c[j][i] : c[j][i] & ((1u << (8 * uint32_t(len - q))) - 1u);
-                }
-            }
-        }
-        nb += NB;
-    }
-};
-
-// Snk whose whole 64-byte blocks are stored by the wave together: lane l's realigned block goes to
-// row l of a 4 KiB per-wave exchange, and store instruction q writes the blocks of lanes 16q ..
-// 16q+15, four lanes (16 bytes each) per block -- 16 destinations per instruction instead of 64
-// scattered 16-byte pieces (the texture path's cost that BlockSrcW removes on the load side).  A
-// lane's first block and its partial last one go through Snk's byte-exact path on their own.
-// Contract: every lane calls init() and put16() in uniform control flow; the b-th put16() call
-// (b = 0, 1, ...) carries output bytes [64 b, 64 b + 64) of a lane that has them (act), so output
-// block b of lane r sits at r's first dword + 16 b (Snk advances one dword per chunk on both paths).
-struct SnkW {
-    Snk s;
-    uint8_t *xw;
-    uint32_t lane;
-    uint64_t qa[4];      // address of dword 4 (lane & 3) of the first output dword of lane 16q + lane/4
-
-    BRB_DEV void init(uint8_t *a, uint64_t n, uint8_t *exchange)
-    {
-        s.init(a, n);
-        xw = exchange;
-        lane = threadIdx.x & 63;
-        const uint64_t pa = reinterpret_cast<uint64_t>(s.p);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int src = 16 * q + int(lane >> 2);
-            const uint64_t a_r = (uint64_t(uint32_t(__shfl(int(pa >> 32), src))) << 32) | uint32_t(__shfl(int(uint32_t(pa)), src));
-            qa[q] = a_r + 16 * (lane & 3);
-        }
-    }
-
-    BRB_DEV void put16(const uint32_t (&v)[16], uint32_t b, bool act)
-    {
-        const bool fast = act && !s.first && s.rem >= 64;
-        if (act && !fast) {
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-                s.put(v[k]);
-        }
-        // Snk::put16's realignment: out_k = bytes of {v_k : v_{k-1}} shifted by the output offset
-        const uint32_t o = s.o;
-        const uint32_t sel = 0x07060504u - 0x01010101u * o;
-        uint32_t prev = o ? s.carry << (8 * (4 - o)) : 0u;
-        uint32_t w[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            w[k] = __builtin_amdgcn_perm(v[k], prev, sel);
-            prev = v[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            *reinterpret_cast<uint4 *>(xw + BlockSrcW::xoff(lane, k)) = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        const uint64_t m = __ballot(fast);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t r = 16 * q + (lane >> 2);
-            if ((m >> r) & 1) {
-                const uint4 t = *reinterpret_cast<const uint4 *>(xw + BlockSrcW::xoff(r, lane & 3));
-                st16_a4(reinterpret_cast<uint8_t *>(qa[q] + 64ull * b), t.x, t.y, t.z, t.w);
-            }
-        }
-        if (fast) {
-            s.p += 16;
-            s.carry = o ? (v[15] >> (32 - 8 * o)) : 0u;
-            s.carry_n = o;
-            s.rem -= 64;
-        }
-    }
-
-    BRB_DEV void flush() { s.flush(); }
-};
-
 // The 0x80 end marker of MD5 / SHA-1 padding at byte len % 64 of a (zero-filled) tail block.
 BRB_DEV void add_marker(uint32_t (&w)[16], uint64_t len)
 {

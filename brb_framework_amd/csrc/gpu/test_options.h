@@ -15,11 +15,11 @@ enum Opt {
     kDevices = 4,       // 0: BRB_BATCH_ALL_DEVICES / all-devices batchers use every visible device;
                         // k > 0: they split into k parts, part g on device g % (visible devices) --
                         // the concurrent multi-device paths exercised on a one-GPU box
-    kB64Pieces = 5,     // 0: the launcher's choice; 1 / 2: base64 encode lanes per record
+    kB64Group = 5,      // -1: the launcher's choice; 0..6: log2 of the base64 lanes per record
     kCount = 6
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, 0};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

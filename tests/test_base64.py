@@ -52,12 +52,13 @@ def _records(seed, n, max_len):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pieces", [0, 1, 2])
+@pytest.mark.parametrize("group", [-1, 0, 1, 3, 4, 5, 6])
 @pytest.mark.parametrize("seed,n,max_len", [(1, 500, 40), (2, 300, 3000), (3, 20, 100000)])
-def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len, pieces):
-    """pieces: encode lanes per record (test option b64_pieces; 0 = the launcher's choice): with 2,
-    each record is cut into two pieces encoded by two lanes, the first a multiple of 3 bytes."""
-    with brb.TestOption("b64_pieces", pieces):
+def test_encode_decode_batch(brb, orc, torch_dev, seed, n, max_len, group):
+    """group: log2 of the lanes per record (test option b64_group; -1 = the launcher's choice, from
+    the mean length in host mode and 32 lanes in device mode).
+    Records start and end at every byte alignment, inputs and outputs alike."""
+    with brb.TestOption("b64_group", group):
         _encode_decode_batch(brb, orc, torch_dev, seed, n, max_len)
 
 
@@ -108,9 +109,16 @@ def _encode_decode_batch(brb, orc, torch_dev, seed, n, max_len):
 
 
 @pytest.mark.gpu
-def test_decode_falls_back_mid_record(brb, orc):
-    """Long records whose first skipped byte, NUL or '=' run comes after several 256-character
-    fast-path steps: the fast steps' output and the serial remainder must join exactly (base64.c:131-179)."""
+@pytest.mark.parametrize("group", [-1, 0, 2, 5, 6])
+def test_decode_falls_back_mid_record(brb, orc, group):
+    """Long records whose first skipped byte, NUL or '=' run comes after many fixed-position pieces:
+    the pieces' output and the serial remainder must join exactly (base64.c:131-179), and nothing is
+    written past the decoded bytes."""
+    with brb.TestOption("b64_group", group):
+        _decode_falls_back_mid_record(brb, orc)
+
+
+def _decode_falls_back_mid_record(brb, orc):
     rng = np.random.default_rng(9)
     n = 400
     texts = []
