@@ -49,7 +49,7 @@ def dispatches(trace_csv):
 
 
 def regions(rows):
-    """[(kernel name -> [durations ns]) per region between consecutive sentinel pairs]."""
+    """[(kernel name -> [durations ns], in dispatch order) per region between consecutive sentinel pairs]."""
     sent = [(s, e) for s, e, n in rows if SENTINEL in n]
     out = []
     for i in range(0, len(sent) - 1, 2):
@@ -60,6 +60,16 @@ def regions(rows):
                 acc.setdefault(n, []).append(e - s)
         out.append({"span_us": round((hi - lo) / 1e3, 3), "kernels": acc})
     return out
+
+
+def series(v, buckets=16):
+    """Mean duration (us) of consecutive slices of the dispatches, in order: a drift from the first
+    slices to the last shows the clock settling under sustained load."""
+    n = len(v)
+    if n < buckets:
+        return None
+    return [round(sum(v[b * n // buckets:(b + 1) * n // buckets]) / ((b + 1) * n // buckets - b * n // buckets) / 1e3, 2)
+            for b in range(buckets)]
 
 
 def short(name):
@@ -79,7 +89,8 @@ def line_check(line, regs):
             per_step_us = sum(sum(v) / len(v) * len(v) / steps for v in ks.values()) / 1e3
             out = {"timed_dispatches": n, "kernels_per_step": n // steps, "steps": steps,
                    "kernels": {short(k): {"count": len(v), "mean_us": round(sum(v) / len(v) / 1e3, 3),
-                                          "min_us": round(min(v) / 1e3, 3), "max_us": round(max(v) / 1e3, 3)}
+                                          "min_us": round(min(v) / 1e3, 3), "max_us": round(max(v) / 1e3, 3),
+                                          "series_us": series(v)}
                                for k, v in ks.items()},
                    "rocprof_us_per_step": round(per_step_us, 3), "bench_event_us_per_step": event_us,
                    "region_span_us": reg["span_us"]}

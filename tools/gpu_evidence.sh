@@ -4,6 +4,7 @@
 # from the rocprof mean of exactly its timed dispatches.  Each step has its own time limit; a failed
 # step ends the script.
 #   tools/gpu_evidence.sh <tag> [line ...]     (default: every line)
+#   PLAIN=gpurun_out/<tag2> ...: also join the unprofiled lines of tools/gpu_bench_all.sh <tag2>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -24,6 +25,6 @@ for l in $LINES; do
   echo "$l ok"
 done
 timeout -k 10 300 python3 bench.py --config 1 > "$O/cfg1.json" 2> "$O/cfg1.err" && echo "cfg1 ok"
-timeout -k 10 300 python3 tools/collect_evidence.py "$O" "$O/evidence" || exit 1
+timeout -k 10 300 python3 tools/collect_evidence.py "$O" "$O/evidence" $PLAIN || exit 1
 # the raw traces (tens of MB per line) stay on the box; the per-region summaries come back
 find "$O" -name run_kernel_trace.csv -delete
