@@ -3,8 +3,9 @@
 // MetaDataHeaderLoadData (libbrb_core/data/utils/meta_data.c:397-433) digests the items of one
 // MetaData as BRB_MD5Init, one BRB_MD5UpdateBig per item, BRB_MD5Final: the MD5 of the items'
 // concatenation, the items scattered in memory.  Batched: one record (one MetaData) per lane, its
-// segments (items) walked in order in 64-byte blocks (brb_io::BlockSrc, the next block in flight),
-// their bytes funnelled into the lane's MD5 (md5_funnel.h).
+// segments (items) walked in order in 64-byte blocks (brb_io::BlockSrc, the next block in flight,
+// and the next segment's first block in flight while the current one is hashed), their bytes
+// funnelled into the lane's MD5 (md5_funnel.h).
 #include "brb_kernels.h"
 #include "byte_stream.h"
 #include "md5_funnel.h"
@@ -27,18 +28,27 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
     brb_md5::Funnel f;
     f.init(&blk[wave][0][lane]);
     const uint64_t k1 = first[r + 1];
-    for (uint64_t k = first[r]; k < k1; k++) {         // 64-byte blocks, the next one in flight
-        // The segment is read as a range starting e = (bytes digested so far) mod 4 bytes before
-        // it, so its words fall on the digest's word boundaries (as metadata_unpack_kernel): those
-        // e bytes are the carried ones (Funnel::head), never loaded from below the segment.
-        const uint64_t len = slen[k];
-        if (len == 0)                                   // no bytes: its address need not be memory
-            continue;
-        const uint8_t *a = data + soff[k];
+    // Segment k is read as a range starting e_k = (bytes before it) mod 4 bytes before it, so its
+    // words fall on the digest's word boundaries (as metadata_unpack_kernel): those e bytes are the
+    // carried ones (Funnel::head), never loaded from below the segment.  e_k depends only on the
+    // lengths, so segment k + 1's source starts (its first block in flight) before segment k is
+    // hashed: the two sources alternate (sa, sb: no register copies), and a segment's first block no
+    // longer waits a whole HBM round trip after the previous segment's last one.
+    uint64_t k = first[r], before = 0;
+    auto skip_empty = [&](uint64_t kk) {                // the next segment with bytes (an empty one's
+        while (kk < k1 && slen[kk] == 0)                // address need not be memory)
+            kk++;
+        return kk;
+    };
+    auto start = [&](brb_io::BlockSrc &src, uint64_t kk, uint64_t pre, uint64_t &len) {
+        len = slen[kk];
+        const uint8_t *a = data + soff[kk];
+        const uint32_t e = uint32_t(pre & 3);
+        src.init(a - e, len + e, a);
+    };
+    auto run = [&](brb_io::BlockSrc &src, uint64_t len) {   // 64-byte blocks, the next one in flight
         const uint32_t e = f.nacc;
         const uint64_t n = len + e;
-        brb_io::BlockSrc src;
-        src.init(a - e, n, a);
         for (uint64_t c = 0; c < n; c += 64) {
             uint32_t w[16];
             src.fetch(w);
@@ -56,6 +66,25 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
             f.nacc = 0;
         }
         f.total += len;
+    };
+    brb_io::BlockSrc sa, sb;
+    uint64_t la = 0, lb = 0;
+    k = skip_empty(k);
+    if (k < k1)
+        start(sa, k, before, la);
+    while (k < k1) {
+        uint64_t kb = skip_empty(k + 1);
+        if (kb < k1)
+            start(sb, kb, before + la, lb);
+        run(sa, la);
+        before += la;
+        if (kb >= k1)
+            break;
+        k = skip_empty(kb + 1);
+        if (k < k1)
+            start(sa, k, before + lb, la);
+        run(sb, lb);
+        before += lb;
     }
     const Md5State st = f.finish();
     const uint4 v = make_uint4(st.a, st.b, st.c, st.d);
