@@ -9,7 +9,8 @@
 // Output per configuration: kernel time (hipEvent, best of 3), lane-compressions per SIMD per
 // microsecond, shader cycles per wave-instruction per SIMD (clock from s_memtime / s_memrealtime),
 // and the overlap of the waves' lifetimes (1.0 = all resident together).
-// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../brb_framework_amd/csrc/gpu -I../../include \
+// Also SHA-1 (sha1_device.h) and the all-fast MD5 variant (md5_split).  Build (not through head/pipes:
+// a SIGPIPE kills hipcc): hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../brb_framework_amd/csrc/gpu -I../../include \
 //          md5_occ.hip -o md5_occ
 #include <hip/hip_runtime.h>
 
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "md5_device.h"
+#include "sha1_device.h"
 
 // Split-add step (all-fast-ops variant): x = a + (m + K) and y = x + F as plain v_add_u32 (inline asm
 // keeps hipcc from fusing them into v_add3_u32), so a step is 5 fast ops + 1 v_alignbit_b32.
@@ -64,8 +66,10 @@ BRB_DEV void md5_split(Md5State &st, const uint32_t (&m)[16])
 
 constexpr int ITERS = 400;
 constexpr double VALU_PER_ITER = 326.0;     // hipcc -S: 325 in md5_compress + the xor below
+constexpr double VALU_PER_ITER_SPLIT = 390.0;   // md5_split: 64 more v_add_u32 (hipcc -S)
+constexpr double VALU_PER_ITER_SHA1 = 600.0;     // sha1_compress + the xor (hipcc -S, loop body)
 
-template <int A, bool SPLIT>
+template <int A, int KIND>
 __global__ __launch_bounds__(256) void md5_loop(uint32_t *out, unsigned long long *t, uint32_t seed)
 {
     const unsigned lane = threadIdx.x & 63;
@@ -74,20 +78,26 @@ __global__ __launch_bounds__(256) void md5_loop(uint32_t *out, unsigned long lon
     for (int i = 0; i < 16; i++)
         m[i] = seed * (i + 1) + threadIdx.x * 7919u + blockIdx.x;
     Md5State st = md5_iv();
+    Sha1State s1 = sha1_iv();
     const unsigned long long c0 = __builtin_amdgcn_s_memtime();
     const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     if (lane < unsigned(A)) {
         for (int it = 0; it < ITERS; it++) {
-            if constexpr (SPLIT)
-                md5_split(st, m);
-            else
-                md5_compress<true>(st, m);
-            m[it & 15] ^= st.a;                 // keeps the iterations dependent
+            if constexpr (KIND == 2) {
+                sha1_compress(s1, m);
+                m[it & 15] ^= s1.a;
+            } else {
+                if constexpr (KIND == 1)
+                    md5_split(st, m);
+                else
+                    md5_compress<true>(st, m);
+                m[it & 15] ^= st.a;             // keeps the iterations dependent
+            }
         }
     }
     const unsigned long long c1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
-    out[blockIdx.x * blockDim.x + threadIdx.x] = st.a ^ st.b ^ st.c ^ st.d;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = st.a ^ st.b ^ st.c ^ st.d ^ s1.a ^ s1.e;
     if (lane == 0) {
         const unsigned w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
         t[4 * w + 0] = c0;
@@ -97,8 +107,8 @@ __global__ __launch_bounds__(256) void md5_loop(uint32_t *out, unsigned long lon
     }
 }
 
-template <int A, bool SPLIT = false>
-int run(int W, int cus)
+template <int A, int KIND = 0>
+int run(int W, int cus, double valu_per_iter)
 {
     const int blocks = cus * W;                 // 4-wave blocks: W waves per SIMD
     const int nw = blocks * 4;
@@ -112,7 +122,7 @@ int run(int W, int cus)
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {         // rep 0 warms up
         CK(hipEventRecord(e0));
-        md5_loop<A, SPLIT><<<dim3(blocks), dim3(256)>>>(o, t, 2u + rep);
+        md5_loop<A, KIND><<<dim3(blocks), dim3(256)>>>(o, t, 2u + rep);
         CK(hipEventRecord(e1));
         CK(hipDeviceSynchronize());
         float ms = 0;
@@ -136,10 +146,10 @@ int run(int W, int cus)
     const double overlap = real / double(rmax - rmin);        // 1.0: every wave alive for the whole span
     const double simd_us = best * 1e3;
     const double lane_comp = double(W) * A * ITERS;           // per SIMD
-    const double cpi_simd = simd_us * 1e-6 * ghz * 1e9 / (double(W) * ITERS * VALU_PER_ITER);
-    printf("%s W=%d A=%2d  kernel %8.1f us  %7.1f lane-compressions/us/SIMD  %.2f cycles/wave-instr/SIMD  "
+    const double cpi_simd = simd_us * 1e-6 * ghz * 1e9 / (double(W) * ITERS * valu_per_iter);
+    printf("%s W=%d A=%2d  %.2f ns/instr/SIMD  kernel %8.1f us  %7.1f lane-compressions/us/SIMD  %.2f cycles/wave-instr/SIMD  "
            "%.1f cycles/compress/wave  clock %.2f GHz  overlap %.2f\n",
-           SPLIT ? "split" : "fused", W, A, simd_us, lane_comp / simd_us, cpi_simd, cyc / ITERS, ghz, overlap);
+           KIND == 2 ? "sha1 " : KIND == 1 ? "split" : "fused", W, A, simd_us * 1e3 / (double(W) * ITERS * valu_per_iter), simd_us, lane_comp / simd_us, cpi_simd, cyc / ITERS, ghz, overlap);
     hipFree(o);
     hipFree(t);
     return 0;
@@ -150,8 +160,9 @@ int main()
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     for (int W : {1, 2, 4}) {
-        if (run<64>(W, cus)) return 1;
-        if (run<64, true>(W, cus)) return 1;
+        if (run<64, 0>(W, cus, VALU_PER_ITER)) return 1;
+        if (run<64, 1>(W, cus, VALU_PER_ITER_SPLIT)) return 1;
+        if (run<64, 2>(W, cus, VALU_PER_ITER_SHA1)) return 1;
     }
     return 0;
 }
