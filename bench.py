@@ -42,8 +42,10 @@ CLOCK_GHZ = 2.1                # shader clock the chip holds with every CU issui
                                # profiles/r02d_md5_tput.txt); 2.4 GHz is the maximum, held only with
                                # a few CUs busy (MI355X_MICROARCH.md "DVFS give-back")
 VALU_PEAK_CYC = 2.0            # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (guide, "SIMD")
-LONE_WAVE_CYC = {"md5": 4.85, "sha1": 4.54}   # one wave per SIMD: measured issue cost per VALU
-                                              # instruction (tools/mb/valu_latency.hip)
+LONE_WAVE_CYC = {"md5": 4.30, "sha1": 4.32}   # one wave per SIMD: shader cycles per VALU instruction
+                                              # of the product's own compression at the measured clock
+                                              # (tools/mb/md5_occ.hip, profiles/r03/md5_sha1_occ.txt;
+                                              # round 2's 4.85 / 4.54 were a dependent synthetic chain)
 
 
 def parse():
@@ -134,11 +136,11 @@ def traffic_fields(path, key, per_step=1):
 def compute_fraction(path, key, launch_s, cyc_lone):
     """roofline.compute: the VALU-issue ceiling.  insts = SQ_INSTS_VALU per dispatch (rocprofv3
     --pmc, chip-wide sum of wave-instructions); per SIMD = insts / 1024.  frac_peak = that many
-    instructions at the SIMD's peak issue (2 cycles per wave64 instruction) and 2.4 GHz over the
-    launch time; frac_lone_wave = the same at the cost per instruction measured for the kernel's
-    step mix at one wave per SIMD (tools/mb/valu_latency.hip).  That cost is close to the SIMD's
-    rate for the mix at any wave count: MD5 hashing alone runs 23.4 us at one wave per SIMD and
-    22.0 us at eight (tools/mb/small_probe.hip), so it is the compute ceiling of cfg3/cfg5 too."""
+    instructions at the SIMD's peak issue (2 cycles per wave64 instruction) and CLOCK_GHZ over the
+    launch time; frac_lone_wave = the same at the cost per instruction measured for the product's
+    compression at one wave per SIMD (tools/mb/md5_occ.hip).  That cost is close to the SIMD's
+    rate for the mix at any wave count (4.30 / 4.11 / 4.03 cycles at 1 / 2 / 4 waves per SIMD),
+    so it is the compute ceiling of cfg3/cfg5 too."""
     _, det = load_pmc(path, key)
     if not det or "sq_insts_valu" not in det:
         return None
@@ -151,8 +153,8 @@ def compute_fraction(path, key, launch_s, cyc_lone):
     if cyc_lone:
         out["lone_wave_cycles_per_inst"] = cyc_lone
         out["frac_lone_wave"] = round(per_simd * cyc_lone / cyc, 4)
-        out["note"] = ("frac_lone_wave: VALU per SIMD x the step mix's measured cycles per instruction "
-                       "(one wave per SIMD; eight waves per SIMD hash only ~6% faster) / launch cycles at 2.4 GHz")
+        out["note"] = ("frac_lone_wave: VALU per SIMD x the compression's measured cycles per instruction at "
+                       "one wave per SIMD (four waves per SIMD run it only ~7% faster) / launch cycles at clock_ghz")
     return out
 
 
