@@ -178,3 +178,75 @@ def test_full_shape_round_trip(brb, torch_dev):
                                     t.from_numpy(offs).cuda())
     assert (olens.cpu().numpy() == L).all()
     assert np.array_equal(back.cpu().numpy(), data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", [-1, 0, 3, 5, 6])
+def test_group_kernels_fuzz(brb, orc, torch_dev, group):
+    """Many small batches of mixed lengths through the group kernels (test option b64_group): the
+    piece boundaries of encode (12 bytes) and decode (16 characters) against every tail length,
+    records of 0..200 bytes mixed with a few long ones in one group, every input and output byte
+    alignment, device and host mode; bytes between the outputs stay untouched."""
+    rng = np.random.default_rng(77 + group)
+    t = torch_dev
+    with brb.TestOption("b64_group", group):
+        for trial in range(6):
+            n = int(rng.integers(1, 300))
+            lens = rng.integers(0, 200, n).astype(np.uint32)
+            lens[rng.integers(0, n, max(1, n // 30))] = rng.integers(1000, 5000, max(1, n // 30))
+            offs = np.zeros(n, np.uint64)
+            pos = int(rng.integers(0, 4))
+            for i in range(n):
+                offs[i] = pos
+                pos += int(lens[i]) + int(rng.integers(0, 5))
+            data = rng.integers(0, 256, pos + 8, dtype=np.uint8)
+            want = [orc.b64_encode(data[int(o):int(o) + int(L)].tobytes()) for o, L in zip(offs, lens)]
+            elens = np.array([len(w) for w in want], np.uint32)
+            eoffs = np.zeros(n, np.uint64)
+            p = int(rng.integers(0, 4))
+            for i in range(n):
+                eoffs[i] = p
+                p += int(elens[i]) + 1 + int(rng.integers(0, 3))
+            total = p + 8
+            dev = trial % 2 == 1
+            if dev:
+                o = t.full((total,), 0xA5, dtype=t.uint8, device="cuda")
+                brb.base64_encode_batch(t.from_numpy(data).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
+                                        o, t.from_numpy(eoffs).cuda())
+                out = o.cpu().numpy()
+            else:
+                out = np.full(total, 0xA5, np.uint8)
+                brb.base64_encode_batch(data, offs, lens, out, eoffs)
+            mask = np.ones(total, bool)
+            for i in range(n):
+                a, L = int(eoffs[i]), int(elens[i])
+                assert out[a:a + L].tobytes() == want[i], (trial, i, int(lens[i]))
+                mask[a:a + L] = False
+            assert (out[mask] == 0xA5).all()
+            # decode back, with a few skipped bytes / NULs planted in some records
+            text = out.copy()
+            for i in rng.integers(0, n, max(1, n // 10)):
+                if elens[i] > 2:
+                    text[int(eoffs[i]) + int(rng.integers(0, elens[i]))] = int(rng.choice([0, 10, 33, 61]))
+            cap = 3 * (elens // 4)
+            doffs = np.zeros(n, np.uint64)
+            q = int(rng.integers(0, 4))
+            for i in range(n):
+                doffs[i] = q
+                q += int(cap[i]) + 1
+            if dev:
+                d = t.full((q + 8,), 0x5A, dtype=t.uint8, device="cuda")
+                dl = brb.base64_decode_batch(t.from_numpy(text).cuda(), t.from_numpy(eoffs).cuda(),
+                                             t.from_numpy(elens).cuda(), d, t.from_numpy(doffs).cuda())
+                dec, dl = d.cpu().numpy(), dl.cpu().numpy()
+            else:
+                dec = np.full(q + 8, 0x5A, np.uint8)
+                dl = brb.base64_decode_batch(text, eoffs, elens, dec, doffs)
+            dmask = np.ones(q + 8, bool)
+            for i in range(n):
+                w = orc.b64_decode(text[int(eoffs[i]):int(eoffs[i]) + int(elens[i])].tobytes())
+                assert int(dl[i]) == len(w), (trial, i)
+                a = int(doffs[i])
+                assert dec[a:a + len(w)].tobytes() == w, (trial, i)
+                dmask[a:a + len(w)] = False
+            assert (dec[dmask] == 0x5A).all()
