@@ -90,7 +90,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void digest_line3_kernel(const uint8
     auto issue = [&](const uint32_t (&vq)[8], const brb_dma::v4i &rs, uint32_t &so, uint32_t slot, bool keep_l2) {
         const uint32_t m = lds0 + slot * SLOT;
         uint32_t keep;
-        so = __builtin_amdgcn_readfirstlane(so);               // an SGPR, never a literal soffset
+        const uint32_t sso = __builtin_amdgcn_readfirstlane(so);   // an SGPR, never a literal soffset
 #define BRB_LINE3_DMA8(POL)                                                                     \
     asm volatile("s_mov_b32 %0, m0\n\t"                                                          \
                  "s_mov_b32 m0, %10\n\t"                                                         \
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void digest_line3_kernel(const uint8
                  "s_mov_b32 m0, %0"                                                               \
                  : "=&s"(keep)                                                                    \
                  : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "v"(vq[4]), "v"(vq[5]), "v"(vq[6]), \
-                   "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u), "s"(so)                           \
+                   "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u), "s"(sso)                          \
                  : "memory")
         if (keep_l2)
             BRB_LINE3_DMA8("");

@@ -51,13 +51,16 @@ int main(int argc, char **argv)
     uint8_t *o;
     CK(hipMalloc(&o, n * 16));
     const uint64_t groups = (n + 63) / 64;
-    struct V { const char *name; Kern k; int rot; int wg; int line3; };
-    V vs[] = {{"md5   HBM (7 copies)", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, nrot, 8, 0},
-              {"md5   MALL (1 copy) ", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 1, 8, 0},
-              {"stage HBM (7 copies)", brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, nrot, 8, 0},
-              {"stage MALL (1 copy) ", brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 1, 8, 0},
-              {"md5   HBM line3     ", brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, nrot, 4, 1},
-              {"md5   MALL line3    ", brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, 1, 4, 1}};
+    struct V { const char *name; const void *k; int rot; int wg; int line3; };
+    V vs[] = {{"md5   HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, nrot, 8, 0},
+              {"md5   MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 1, 8, 0},
+              {"stage HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, nrot, 8, 0},
+              {"stage MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 1, 8, 0},
+              {"md5   HBM line3     ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, nrot, 4, 1},
+              {"md5   MALL line3    ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, 1, 4, 1},
+              {"md5   HBM line3 late", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, false>, nrot, 4, 1},
+              {"stage HBM line3     ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgNull, 4, true, true>, nrot, 4, 1},
+              {"stage MALL line3    ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgNull, 4, true, true>, 1, 4, 1}};
     const int nv = int(sizeof(vs) / sizeof(vs[0]));
     std::vector<std::vector<float>> us(nv);
     hipEvent_t a, b;
@@ -71,8 +74,13 @@ int main(int argc, char **argv)
             const unsigned g2 = v.line3 ? grid : unsigned(std::min<uint64_t>(groups, 256));
             for (int rep = 0; rep < 2; rep++) {      // rep 0 warms the clock and the cache
                 hipEventRecord(a);
-                for (int i = 0; i < 2000; i++)
-                    hipLaunchKernelGGL(v.k, dim3(g2), dim3(64 * v.wg), 0, 0, d[(it++) % v.rot], L, n, o);
+                for (int i = 0; i < 2000; i++) {
+                    const uint8_t *src = d[(it++) % v.rot];
+                    uint32_t l = L;
+                    uint64_t nn = n;
+                    void *args[] = {&src, &l, &nn, &o};
+                    CK(hipLaunchKernel(v.k, dim3(g2), dim3(64 * v.wg), args, 0, 0));
+                }
                 hipEventRecord(b);
                 CK(hipEventSynchronize(b));
                 float ms;

@@ -65,6 +65,12 @@ struct AlgNull : AlgLit {
 };
 
 using Kern = void (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *);
+// launches a kernel of the four arguments (data, rec_len, n_rec, out)
+static void launch(const void *k, unsigned grid, unsigned bs, const uint8_t *src, uint32_t L, uint64_t n, uint8_t *o)
+{
+    void *args[] = {&src, &L, &n, &o};
+    if (hipLaunchKernel(k, dim3(grid), dim3(bs), args, 0, 0) != hipSuccess) { printf("launch failed\n"); exit(1); }
+}
 
 static double pct(std::vector<double> v, double p)
 {
@@ -89,24 +95,24 @@ int main(int argc, char **argv)
     CK(hipMalloc(&pr, 4096 * NP * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
     struct V { const char *name; Kern k; };
-    struct VG { const char *name; Kern k; int waves; };
-    VG vs64[] = {{"DMA64 static 4x4", brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4},
-                 {"DMA64 dyn16", brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
-                 {"DMA64 dyn8", brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
-                 {"DMA64 only", brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
+    struct VG { const char *name; const void *k; int waves; };
+    VG vs64[] = {{"DMA64 static 4x4", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4},
+                 {"DMA64 dyn16", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
+                 {"DMA64 dyn8", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
+                 {"DMA64 only", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
     // waves = -4: digest_line1_kernel (one group per wave, 4-wave workgroups, grid = groups / 4)
-    VG vs[] = {{"LINE md5 nt dyn8", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
-              {"LINE1 ns3", brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
-              {"LINE1 ns2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
-              {"LINE1 ns2 u4", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
-              {"LINE1 ns3 spread", brb_digest::digest_line1_kernel<AlgLit, true, true, 3, true>, -4},
-              {"LINE1 ns2 spread", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, true>, -4},
-              {"LINE md5 nt dyn8 #2", brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
-              {"LINE1 ns3 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
-              {"LINE1 ns2 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
-              {"LINE1 ns2 u4 #2", brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
-              {"LINE1 dma-only ns3", brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
-              {"LINE dma-only nt dyn8", brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8}};
+    VG vs[] = {{"LINE md5 nt dyn8", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE1 ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
+              {"LINE1 ns2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
+              {"LINE1 ns2 u4", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
+              {"LINE1 ns3 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3, true>, -4},
+              {"LINE1 ns2 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, true>, -4},
+              {"LINE md5 nt dyn8 #2", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE1 ns3 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
+              {"LINE1 ns2 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
+              {"LINE1 ns2 u4 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
+              {"LINE1 dma-only ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
+              {"LINE dma-only nt dyn8", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8}};
     int it = 0;
     const bool small = L <= 64;
     const int nv = small ? 4 : int(sizeof(vs) / sizeof(vs[0]));
@@ -125,16 +131,16 @@ int main(int argc, char **argv)
         float tot = 0;
         while (tot < 500.f) {
             hipEventRecord(a);
-            for (int i = 0; i < 50; i++) hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+            for (int i = 0; i < 50; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
             hipEventRecord(b);
             CK(hipEventSynchronize(b));
             float ms;
             hipEventElapsedTime(&ms, a, b);
             tot += ms;
         }
-        for (int i = 0; i < 9; i++) hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+        for (int i = 0; i < 9; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
         CK(hipMemsetAsync(pr, 0, 4096 * NP * 8));
-        hipLaunchKernelGGL(v.k, dim3(grid), dim3(bs), 0, 0, d[it++ % nrot], L, n, o);
+        launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
         CK(hipDeviceSynchronize());
         std::vector<uint64_t> all(4096 * NP), hp;
         CK(hipMemcpy(all.data(), pr, all.size() * 8, hipMemcpyDeviceToHost));
@@ -168,6 +174,19 @@ int main(int argc, char **argv)
             for (double q : {0.0, 0.1, 0.25, 0.5, 0.75, 0.9, 0.95, 0.99, 1.0}) printf(" p%g=%.1f", q * 100, pct(en, q));
             std::vector<double> by_slot[2];
             for (uint64_t w = 0; w < nw; w++) by_slot[widx[w] / 1024 % 2].push_back(en[w]);
+            {   // per workgroup (CU): latest and earliest wave end
+                std::vector<double> wmax(4096, 0.0), wmin(4096, 1e30), spread, maxs;
+                const int wpb = v.waves < 0 ? 4 : v.waves;
+                for (uint64_t w = 0; w < nw; w++) {
+                    const uint64_t b = widx[w] / wpb;
+                    wmax[b] = std::max(wmax[b], en[w]);
+                    wmin[b] = std::min(wmin[b], en[w]);
+                }
+                for (int b = 0; b < 4096; b++)
+                    if (wmax[b] > 0) { maxs.push_back(wmax[b]); spread.push_back(wmax[b] - wmin[b]); }
+                printf("\n  per-WG last end p0 %.1f p50 %.1f p100 %.1f | per-WG end spread p10 %.1f p50 %.1f p90 %.1f", pct(maxs, 0),
+                       pct(maxs, .5), pct(maxs, 1), pct(spread, .1), pct(spread, .5), pct(spread, .9));
+            }
             printf("\n  WG<256 end p50 %.1f p90 %.1f | WG>=256 end p50 %.1f p90 %.1f\n", pct(by_slot[0], .5), pct(by_slot[0], .9),
                    by_slot[1].empty() ? 0.0 : pct(by_slot[1], .5), by_slot[1].empty() ? 0.0 : pct(by_slot[1], .9));
         }
