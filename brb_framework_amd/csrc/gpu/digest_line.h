@@ -168,6 +168,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // check covers voffset + soffset + the instruction offset, per dword: tools/mb/buf_range.hip).
     uint32_t so = 0, son = 0;
     auto issue = [&](const uint32_t (&vq)[8], const brb_dma::v4i &rs, uint32_t &so, uint32_t slot, bool keep_l2 = false) {   // next line -> slot
+#ifdef BRB_LINE_NO_DMA      // diagnostic builds only (tools/mb/line_parts.hip): hash stale LDS
+        return;
+#endif
         const uint32_t m = lds0 + slot * SLOT;
         uint32_t keep;
 #define BRB_LINE_DMA8(POL)                                                                      \
@@ -220,6 +223,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
 
     uint32_t w0[16], w1[16];
     auto read_window = [&](const uint32_t (&ad)[32]) {
+#ifdef BRB_LINE_NO_READ     // diagnostic builds only: hash the previous window again
+        return;
+#endif
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             w0[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
