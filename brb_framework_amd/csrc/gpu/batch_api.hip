@@ -1009,8 +1009,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
                  {"var_sort", brb_opt::kVarSort, 0, 2},
                  {"devices", brb_opt::kDevices, 0, 64},
-                 {"b64_group", brb_opt::kB64Group, -1, 6},
-                 {"line3", brb_opt::kLine3, -1, 2}};
+                 {"b64_group", brb_opt::kB64Group, -1, 6}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

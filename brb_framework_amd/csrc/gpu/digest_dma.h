@@ -11,7 +11,6 @@
 #pragma once
 
 #include "digest_line.h"
-#include "digest_line3.h"
 #include "digest_var_line.h"
 #include "dma_stage.h"
 
@@ -215,14 +214,8 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
     // 4-byte record bases and lengths over 64 B: line-aligned staging, digest_line.h (every line
     // is read once; no 128-byte piece straddles two lines).  1 Mi x 1500 B: 343 -> 300 us,
     // cfg2: 25.3 -> 24.9 us (tools/mb/md5_ab.hip).
-    if (line_supported(data, rec_len)) {
-        // the three-slot pipelined-window kernel (digest_line3.h) is an A/B option: on cfg2 it
-        // measured 22.5 us (reads overlapped) / 22.1 us (not) against 21.0 us for this one
-        const int l3 = brb_opt::get(brb_opt::kLine3);
-        if (l3 >= 1)
-            return launch_fixed_line3<Alg>(data, rec_len, n_rec, out, out_al, s, l3 != 2);
+    if (line_supported(data, rec_len))
         return launch_fixed_line<Alg>(data, rec_len, n_rec, out, out_al, s);
-    }
     if (rec_len > 64 && rec_len <= (1u << 20) && fixed_var_line_enabled())
         return launch_fixed_var_line<Alg>(data, rec_len, n_rec, out, out_al, s);   // any byte alignment
     if (rec_len > 64) {

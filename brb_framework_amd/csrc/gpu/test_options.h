@@ -16,12 +16,10 @@ enum Opt {
                         // k > 0: they split into k parts, part g on device g % (visible devices) --
                         // the concurrent multi-device paths exercised on a one-GPU box
     kB64Group = 5,      // -1: the launcher's choice; 0..6: log2 of the base64 lanes per record
-    kLine3 = 6,         // -1/0: 4-byte-aligned fixed-stride digests on digest_line_kernel; 1/2: on the
-                        // three-slot kernel of digest_line3.h with / without the overlapped window reads
-    kCount = 7
+    kCount = 6
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, -1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -374,8 +374,7 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * (variable-length batches bucketed by length / in caller order; 2 keeps the first round of groups in
  * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k parts,
  * part g on device g % count), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
- * forced to 2^value), "line3" -1/0/1/2 (4-byte-aligned fixed-stride digests on the two-slot line kernel /
- * the same / the three-slot kernel with overlapped window reads / without).  Returns 1 and the previous
+ * forced to 2^value).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

@@ -191,31 +191,24 @@ def test_cfg5_host_all_devices(brb, orc, golden):
         assert got[e["r"]].tobytes().hex() == e["md5"]
 
 
-@pytest.mark.parametrize("line3", [0, 1, 2])
 @pytest.mark.parametrize("n,rec_len,off", [
     (65536, 1500, 0),        # cfg2's shape: one group per wave
-    (65601, 1532, 8),        # t = 60: two padding blocks; partial last group
-    (66000, 1508, 12),       # t = 36
-    (65700, 132, 4),         # K = 2: line 2 is the last line
-    (5000, 68, 4),           # K = 1: no line 2, the window of the prologue is the last one
+    (5000, 68, 4),           # K = 1: the window of the prologue is the last one
     (5000, 128, 0),          # K = 1, t = 0: padding block only
     (5000, 192, 4),          # K = 2, nfull odd, t = 0: the last window's second half unused
-    (300_000, 1500, 0),      # several groups per wave (tickets, next group's window read early)
     (300_001, 260, 8),       # several groups per wave, K = 3
 ])
-def test_line_kernels_three_slot(brb, orc, torch_dev, line3, n, rec_len, off):
-    """Both line-aligned kernels on every shape, whichever the launcher would pick: the two-slot
-    digest_line_kernel (line3 = 0) and the three-slot pipelined-window digest_line3_kernel
-    (line3 = 1), every digest against the oracle."""
+def test_line_kernel_short_groups(brb, orc, torch_dev, n, rec_len, off):
+    """The line-aligned kernel at K = 1 and 2 (two or three lines per record) and with several
+    groups per wave, every digest against the oracle."""
     data = workload.gen_records(0x5EED0013, 0, n, rec_len)
     d = torch_dev.zeros(data.size + 64, dtype=torch_dev.uint8, device="cuda")
     d[off:off + data.size] = to_dev(torch_dev, data)
     view = d[off:off + data.size]
-    with brb.TestOption("line3", line3):
-        assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(),
-                              orc.md5_batch_fixed(data, rec_len, n, threads=16))
-        assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
-                              orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+    assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.md5_batch_fixed(data, rec_len, n, threads=16))
+    assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
 @pytest.mark.parametrize("rec_len", [1500, 1501])

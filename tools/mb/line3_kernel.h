@@ -1,4 +1,4 @@
-// digest_line3.h -- the line-aligned digest kernel of digest_line.h with a THREE-slot LDS ring and
+// line3_kernel.h (tools/mb; measured slower, not in the library) -- the line-aligned digest kernel of digest_line.h with a THREE-slot LDS ring and
 // the window reads software-pipelined behind the compressions.  For batches of at most one group
 // of 64 records per SIMD (cfg2: 65 536 records = 1 024 groups = one wave per SIMD), where no second
 // wave hides a wave's own waits.

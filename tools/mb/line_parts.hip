@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "digest_dma.h"
+#include "line3_kernel.h"
 #include "md5_device.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
