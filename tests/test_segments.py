@@ -79,3 +79,27 @@ def test_segments_empty_and_sub_ranges(brb):
     assert got[0].tobytes() == hashlib.md5(b"").digest()
     assert got[1].tobytes() == hashlib.md5(b"").digest()
     assert got[2].tobytes() == hashlib.md5(pool[10:43].tobytes()).digest()
+
+
+def test_segments_at_buffer_ends(brb, orc, torch_dev):
+    """Segments that start at the device buffer's first byte (a range that would begin up to 3
+    bytes before it) and end at its last byte, in a buffer of exactly the pool's size; 130 records
+    (a partial last wave), lengths 1..200."""
+    rng = np.random.default_rng(17)
+    n_rec = 130
+    pool = workload.gen_records(0x5EED00F5, 0, 1, 20001)
+    counts = rng.integers(1, 6, n_rec)
+    first = np.zeros(n_rec + 1, np.uint64)
+    first[1:] = np.cumsum(counts)
+    nseg = int(first[-1])
+    lens = rng.integers(1, 201, nseg).astype(np.uint32)
+    offs = np.array([rng.integers(0, pool.size - int(n) + 1) for n in lens], np.uint64)
+    ends = rng.random(nseg)
+    offs[ends < 0.2] = 0
+    sel = ends > 0.8
+    offs[sel] = pool.size - lens[sel]
+    want = _want(orc, pool, offs, lens, first)
+    t = torch_dev
+    dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
+                                 t.from_numpy(first).cuda())
+    assert np.array_equal(dev.cpu().numpy(), want)
