@@ -748,22 +748,26 @@ def bench_cfg1(args):
         L.BRB_MD5UpdateBig(ctypes.byref(ctx), buf, len(buf))
         L.BRB_MD5Final(ctypes.byref(ctx))
 
-    def timed(fn, seconds):
-        fn()
+    def timed(fn, seconds, k=None, w=1):
+        """W untimed calls, then exactly K timed ones (--steps / --warmup), or as many as fill
+        `seconds`."""
+        for _ in range(max(1, w)):
+            fn()
         n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
+        while (n < k) if k else (time.perf_counter() - t0 < seconds):
             fn()
             n += 1
         return n, time.perf_counter() - t0
 
-    steps, dt = timed(compat, max(1.0, args.cpu_seconds / 2))
+    warm = args.warmup if args.warmup is not None else 1
+    steps, dt = timed(compat, max(1.0, args.cpu_seconds / 2), args.steps, warm)
     assert bytes(ctx.digest).hex() == want, "compat MD5 of the cfg1 buffer differs from the golden digest"
     o_steps, o_dt = timed(lambda: oracle.md5(buf), max(1.0, args.cpu_seconds / 2))
     assert oracle.md5(buf).hex() == want
     rate = len(buf) * steps / dt / 2**30
     o_rate = len(buf) * o_steps / o_dt / 2**30
     return {"metric": "GiB/s of MD5 over one 1 MiB buffer through the compat BRB_MD5Init/UpdateBig/Final (cfg1, CPU)",
-            "value": round(rate, 3), "unit": "GiB/s", "n_gpus": 0, "steps": steps, "warmup": 1,
+            "value": round(rate, 3), "unit": "GiB/s", "n_gpus": 0, "steps": steps, "warmup": max(1, warm),
             "ms_per_step": round(dt / steps * 1e3, 4), "higher_is_better": True, "scaling": "none",
             "vs_baseline": None, "dtype": "u32", "data": "synthetic (SURVEY §8(d) generator, seed 0x5EED0001)",
             "config": {"workload": cfg["name"], "op": "BRB_MD5Init + BRB_MD5UpdateBig + BRB_MD5Final (compat, host C)",
