@@ -35,8 +35,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s (device-resident) + Mrecords/s over 1500B buffers at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
-TIMING = ("HIP events on the launch stream from the end of step 1 to the end of step K, / (K-1): back-to-back "
-          "launches without the first launch's host-to-GPU latency (the wall time behind `value` includes it)")
+TIMING = ("HIP events on the launch stream from the end of step 2 to the end of step K, / (K-2): back-to-back "
+          "launches without the first two after the idle synchronize (the wall time behind `value` includes them)")
 L3_BYTES = 256 << 20
 SIMDS = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.1                # shader clock the chip holds with every CU issuing these kernels:
@@ -285,18 +285,20 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     host enqueues faster than the GPU drains).  Returns (wall seconds max over ranks, seconds per
     launch from HIP events on the launch stream).
 
-    The per-launch time is what roofline.achieved divides by.  On one stream with K >= 2 the event
-    pair brackets steps 2..K (e0 is enqueued right after step 1, so it fires when step 1 ends and
-    step 2 starts; e1 fires when step K ends): K-1 back-to-back launches, without the host-to-GPU
-    latency of the first launch, which the wall time (and so `value`) still includes.  Measured
-    with the driver's --steps 20 --warmup 5: the bracket over all K steps read 22.5 us per cfg2
-    launch against 21.2 us for the same dispatches in rocprof.  Nothing is enqueued between
-    kernels."""
+    The per-launch time is what roofline.achieved divides by.  On one stream with K >= 3 the event
+    pair brackets steps 3..K: e0 is enqueued right after step 2 (it fires when step 2 ends), e1
+    when step K ends -- K-2 back-to-back launches.  Left out: the host-to-GPU latency of the first
+    launch, and the first two launches after the idle synchronize, which run 15-25 % slower (a
+    20-step region under rocprofv3: 25.2 and 27.2 us, then 21.5-22.8 us).  Recording e0 after step
+    2 rather than step 1 also keeps the host's event call off the critical path: enqueued between
+    steps 1 and 2 it left a 5.6 us gap between the two kernels.  The wall time (and so `value`)
+    covers all K steps.  Nothing is enqueued between kernels.
+    """
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if MARK:             # sentinel before the region, drained before t0
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
-    steady = len(streams) == 1 and n_steps >= 2
+    steady = len(streams) == 1 and n_steps >= 3
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -305,7 +307,7 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     for k in range(n_steps):
         j = k % len(streams)
         launch(k, streams[j], j)
-        if steady and k == 0:
+        if steady and k == 1:
             e0.record(streams[0])
     e1.record(streams[0])
     torch.cuda.synchronize()
@@ -315,7 +317,7 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
             torch.cuda._sleep(1)
         torch.cuda.synchronize()
     wall = max_over_ranks(time.perf_counter() - t0)
-    return wall, e0.elapsed_time(e1) / 1e3 / (n_steps - 1 if steady else n_steps)
+    return wall, e0.elapsed_time(e1) / 1e3 / (n_steps - 2 if steady else n_steps)
 
 
 def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log):

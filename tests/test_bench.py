@@ -50,26 +50,26 @@ def _fake_torch(clock, kernel_ms):
     return types.SimpleNamespace(cuda=cuda)
 
 
-def test_timed_steps_covers_launches_2_to_k():
-    """One stream: e0 is recorded right after launch 1 (it fires when launch 1 ends), e1 after
-    launch K, so the per-launch time is (launches 2..K) / (K - 1); the first launch's extra
-    host-to-GPU latency (modelled as a 50 ms stall) stays out of it."""
+def test_timed_steps_covers_launches_3_to_k():
+    """One stream: e0 is recorded right after launch 2 (it fires when launch 2 ends), e1 after
+    launch K, so the per-launch time is (launches 3..K) / (K - 2); the first launches' extra time
+    (modelled as 50 ms and 20 ms stalls) stays out of it."""
     clock = _Clock()
     torch = _fake_torch(clock, 2.0)
 
     def launch(k, s, j):
         clock.log.append(f"launch{k}")
-        clock.t += 2.0 + (50.0 if k == 0 else 0.0)
+        clock.t += 2.0 + (50.0 if k == 0 else 20.0 if k == 1 else 0.0)
 
     bench.MARK = False
     wall, per = bench.timed_steps(launch, 5, ["s0"], lambda: None, lambda x: x, torch)
-    assert clock.log == ["launch0", "event", "launch1", "launch2", "launch3", "launch4", "event"]
+    assert clock.log == ["launch0", "launch1", "event", "launch2", "launch3", "launch4", "event"]
     assert abs(per - 2.0e-3) < 1e-12          # seconds per launch
     assert wall >= 0
 
 
 def test_timed_steps_multi_stream_brackets_all():
-    """Several streams (or K = 1): the events bracket every launch and the time is divided by K."""
+    """Several streams (or K < 3): the events bracket every launch and the time is divided by K."""
     clock = _Clock()
     torch = _fake_torch(clock, 2.0)
 
