@@ -462,3 +462,51 @@ def _covered(offs, lens, total):
     for o, n in zip(offs.tolist(), lens.tolist()):
         m[o:o + n] = True
     return m
+
+
+@pytest.mark.gpu
+def test_streams_beyond_4gib(brb, orc, torch_dev):
+    """Stream and record offsets past 2^32 in one 4.5 GiB device buffer: 600 streams (0..3000 bytes,
+    some straddling byte offsets 2^31 and 2^32, some ending at the buffer's last byte) through the
+    variable-length MD5 batch and the RC4 pass (in place), against hashlib and the oracle on host
+    copies of just those streams; states included."""
+    torch = torch_dev
+    total = 9 << 29
+    words = torch.empty(total // 8, dtype=torch.int64, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x4B1C)
+    words.random_(generator=g)
+    d = words.view(torch.uint8)
+    rng = np.random.default_rng(11)
+    n = 600
+    lens = rng.integers(0, 3001, n).astype(np.uint32)
+    offs = rng.integers(0, total - 3001, n).astype(np.uint64)
+    for i, o in enumerate([(1 << 31) - 700, (1 << 32) - 700, (1 << 32) - 1, 1 << 32, (1 << 32) + 3]):
+        offs[i], lens[i] = o, 1500
+    offs[5], lens[5] = total - 1500, 1500
+    offs[6], lens[6] = total - 7, 7
+    # non-overlapping streams (the RC4 pass writes in place): drop any that overlaps an earlier one
+    order = np.argsort(offs, kind="stable")
+    keep, end = [], 0
+    for i in order.tolist():
+        if int(offs[i]) >= end:
+            keep.append(i)
+            end = int(offs[i]) + int(lens[i])
+    keep = np.array(sorted(keep))
+    offs, lens = offs[keep], lens[keep]
+    host = [d[int(o):int(o) + int(m)].cpu().numpy() for o, m in zip(offs, lens)]
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    dig = brb.md5_batch(d, to(offs.view(np.int64)), to(lens.view(np.int32))).cpu().numpy()
+    for i, h in enumerate(host):
+        assert dig[i].tobytes() == hashlib.md5(h.tobytes()).digest(), f"md5 stream {i} at {int(offs[i])}"
+    states = brb.rc4_states(_keys(len(offs), 9))
+    ts = to(states)
+    brb.rc4_crypt_batch(ts, d, to(offs.view(np.int64)), to(lens.view(np.int32)))
+    got_st = ts.cpu().numpy()
+    for i, h in enumerate(host):
+        s2, ob = orc.rc4_crypt(states[i].tobytes(), h.tobytes())
+        o, m = int(offs[i]), int(lens[i])
+        assert d[o:o + m].cpu().numpy().tobytes() == ob, f"rc4 stream {i} at {o}"
+        assert got_st[i].tobytes() == s2, f"rc4 state {i}"
+    del words, d
+    torch.cuda.empty_cache()
