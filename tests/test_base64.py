@@ -250,3 +250,47 @@ def test_group_kernels_fuzz(brb, orc, torch_dev, group):
                 assert dec[a:a + len(w)].tobytes() == w, (trial, i)
                 dmask[a:a + len(w)] = False
             assert (dec[dmask] == 0x5A).all()
+
+
+@pytest.mark.gpu
+def test_beyond_4gib(brb, orc, torch_dev):
+    """Input offsets past 2^32 (encode) and output offsets past 2^32 (decode) in one 4.5 GiB device
+    buffer: 300 records of 0..3000 bytes, some straddling byte offsets 2^31 and 2^32, encoded into
+    a small text buffer (== Python's base64) and decoded back into the big buffer's top 8 MiB (==
+    the oracle's decode, which keeps the reference's length rule: whole 3-byte groups)."""
+    t = torch_dev
+    total = 9 << 29
+    words = t.empty(total // 8, dtype=t.int64, device="cuda")
+    g = t.Generator(device="cuda")
+    g.manual_seed(0x4B1D)
+    words.random_(generator=g)
+    d = words.view(t.uint8)
+    rng = np.random.default_rng(21)
+    n = 300
+    lens = rng.integers(0, 3001, n).astype(np.uint32)
+    offs = rng.integers(0, total - (16 << 20), n).astype(np.uint64)
+    for i, o in enumerate([(1 << 31) - 1000, (1 << 32) - 1000, (1 << 32) - 1, (1 << 32) + 1]):
+        offs[i], lens[i] = o, 2000
+    host = [d[int(o):int(o) + int(m)].cpu().numpy().tobytes() for o, m in zip(offs, lens)]
+    want = [base64.b64encode(h) for h in host]
+    tl = np.array([len(w) for w in want], np.uint32)
+    to = np.zeros(n, np.uint64)
+    to[1:] = np.cumsum(tl.astype(np.uint64))[:-1]
+    text = t.zeros(int(tl.sum()) + 8, dtype=t.uint8, device="cuda")
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    brb.base64_encode_batch(d, dev(offs), dev(lens), text, dev(to))
+    tx = text.cpu().numpy()
+    for i in range(n):
+        assert tx[int(to[i]):int(to[i]) + int(tl[i])].tobytes() == want[i], f"record {i} at {int(offs[i])}"
+    dec = [orc.b64_decode(w) for w in want]
+    dl = np.array([len(x) for x in dec], np.uint64)
+    doffs = np.zeros(n, np.uint64)
+    doffs[1:] = np.cumsum(dl)[:-1]
+    doffs += total - (8 << 20)
+    olens = brb.base64_decode_batch(text, dev(to), dev(tl), d, dev(doffs)).cpu().numpy()
+    for i in range(n):
+        assert int(olens[i]) == len(dec[i]) and dec[i][:len(host[i])] == host[i]
+        o = int(doffs[i])
+        assert d[o:o + len(dec[i])].cpu().numpy().tobytes() == dec[i], f"decoded record {i} at {o}"
+    del words, d
+    t.cuda.empty_cache()

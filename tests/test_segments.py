@@ -103,3 +103,34 @@ def test_segments_at_buffer_ends(brb, orc, torch_dev):
     dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
                                  t.from_numpy(first).cuda())
     assert np.array_equal(dev.cpu().numpy(), want)
+
+
+def test_segments_beyond_4gib(brb, torch_dev):
+    """Segment offsets past 2^32 in one 4.5 GiB device buffer: 500 records of 1..6 segments
+    (0..700 bytes), some straddling byte offsets 2^31 and 2^32, against hashlib on host copies of
+    just those segments."""
+    t = torch_dev
+    total = 9 << 29
+    words = t.empty(total // 8, dtype=t.int64, device="cuda")
+    g = t.Generator(device="cuda")
+    g.manual_seed(0x4B1E)
+    words.random_(generator=g)
+    d = words.view(t.uint8)
+    rng = np.random.default_rng(31)
+    n_rec = 500
+    counts = rng.integers(1, 7, n_rec)
+    first = np.zeros(n_rec + 1, np.uint64)
+    first[1:] = np.cumsum(counts)
+    nseg = int(first[-1])
+    lens = rng.integers(0, 701, nseg).astype(np.uint32)
+    offs = rng.integers(0, total - 701, nseg).astype(np.uint64)
+    for i, o in enumerate([(1 << 31) - 300, (1 << 32) - 300, (1 << 32) - 1, (1 << 32) + 2, total - 700]):
+        offs[i], lens[i] = o, 700
+    segs = [d[int(o):int(o) + int(m)].cpu().numpy().tobytes() for o, m in zip(offs, lens)]
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
+    for i in range(n_rec):
+        msg = b"".join(segs[k] for k in range(int(first[i]), int(first[i + 1])))
+        assert got[i].tobytes() == hashlib.md5(msg).digest(), i
+    del words, d
+    t.cuda.empty_cache()
