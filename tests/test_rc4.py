@@ -510,3 +510,55 @@ def test_streams_beyond_4gib(brb, orc, torch_dev):
         assert got_st[i].tobytes() == s2, f"rc4 state {i}"
     del words, d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_frames_beyond_4gib(brb, orc, torch_dev):
+    """The RC4+MD5 frame and open kernels with payloads read from, and frames written to, byte
+    offsets past 2^31 and 2^32 of one 4.5 GiB device buffer: 300 connections (0..3000-byte
+    payloads), every frame against the oracle's frame, then opened in place (valid, payload back,
+    both ends' states equal)."""
+    torch = torch_dev
+    total = 9 << 29
+    words = torch.empty(total // 8, dtype=torch.int64, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x4B1F)
+    words.random_(generator=g)
+    d = words.view(torch.uint8)
+    rng = np.random.default_rng(41)
+    n = 300
+    lens = rng.integers(0, 3001, n).astype(np.uint32)
+    # payloads in the lower 4 GiB + 256 MiB (some straddling 2^31 / 2^32), frames back to back
+    # (3-byte gaps, odd start) above them, all past 2^32 + 256 MiB
+    offs = rng.integers(0, (1 << 32) + (256 << 20), n).astype(np.uint64)
+    offs[0], offs[1], lens[0], lens[1] = (1 << 31) - 900, (1 << 32) - 900, 2000, 2000
+    foffs = np.zeros(n, np.uint64)
+    foffs[1:] = np.cumsum(lens.astype(np.uint64) + 30 + 3)[:-1]
+    foffs += (1 << 32) + (256 << 20) + 8191
+    # every range inside the buffer (checked on the host before any kernel runs)
+    assert int((offs + lens).max()) <= (1 << 32) + (256 << 20) + 3000 < int(foffs[0])
+    assert int(foffs[-1]) + 30 + int(lens[-1]) <= total
+    payload = [d[int(o):int(o) + int(m)].cpu().numpy().tobytes() for o, m in zip(offs, lens)]
+    salts = np.array([(0x9E3779B9 * (i + 3)) & 0xFFFFFFFF for i in range(n)], np.uint64)
+    keys = _keys(n, 41)
+    states = brb.rc4_states(keys)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    ws, rs = to(states), to(states)
+    brb.rc4md5_frame_batch(ws, d, to(offs.view(np.int64)), to(lens.view(np.int32)), to(salts.view(np.int64)), d,
+                           to(foffs.view(np.int64)))
+    want_st = []
+    for i in range(n):
+        s2, f = orc.rc4md5_frame(states[i].tobytes(), payload[i], int(salts[i]))
+        fo = int(foffs[i])
+        assert d[fo:fo + 30 + int(lens[i])].cpu().numpy().tobytes() == f, f"frame {i} at {fo}"
+        want_st.append(s2)
+    assert ws.cpu().numpy().tobytes() == b"".join(want_st)
+    flens = (lens + 30).astype(np.uint32)
+    _, valid = brb.rc4md5_open_batch(rs, d, to(foffs.view(np.int64)), to(flens.view(np.int32)))
+    assert bool(valid.cpu().numpy().astype(bool).all())
+    assert torch.equal(ws, rs)
+    for i in range(n):
+        fo = int(foffs[i])
+        assert d[fo + 30:fo + 30 + int(lens[i])].cpu().numpy().tobytes() == payload[i], f"opened {i}"
+    del words, d
+    torch.cuda.empty_cache()
