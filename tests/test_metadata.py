@@ -216,3 +216,31 @@ def test_unpack_large_items(brb, orc):
         packs += [p, mutate(rng, items, p)]
     buf, offs, lens = scatter(rng, packs)
     assert infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens)) == [orc.metadata_unpack(p) for p in packs]
+
+
+@pytest.mark.gpu
+def test_unpack_beyond_4gib(brb, orc):
+    """Packs at byte offsets past 2^32: the same 2 000 scattered packs copied into one 4.5 GiB
+    device buffer three times -- straddling 2^31, straddling 2^32, and ending at the buffer's last
+    byte -- and unpacked in one call; every BRB_MetaDataUnpackInfo field equals the oracle's."""
+    import torch
+    packs = corpus(13, 2000)
+    buf, offs, lens = scatter(np.random.default_rng(14), packs)
+    want = [orc.metadata_unpack(p) for p in packs]
+    total = 9 << 29
+    size = buf.size - 1                           # scatter() appends one NUL
+    bases = [(1 << 31) - size // 2, (1 << 32) - size // 2, total - size]
+    assert bases[0] + size <= bases[1] and bases[1] + size <= bases[2] and bases[2] + size == total
+    d = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(buf[:size].copy()).cuda()
+    for b in bases:
+        d[b:b + size] = src
+    all_offs = np.concatenate([offs + np.uint64(b) for b in bases])
+    all_lens = np.concatenate([lens] * 3)
+    assert int((all_offs + all_lens).max()) <= total
+    o = torch.from_numpy(all_offs.view(np.int64)).cuda()
+    ln = torch.from_numpy(all_lens.view(np.int32)).cuda()
+    dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    assert infos_as_tuples(dev) == want * 3
+    del d, src
+    torch.cuda.empty_cache()
