@@ -223,9 +223,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
 
     uint32_t w0[16], w1[16];
     auto read_window = [&](const uint32_t (&ad)[32]) {
-#ifdef BRB_LINE_NO_READ     // diagnostic builds only: hash the previous window again
-        return;
-#endif
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             w0[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
