@@ -216,3 +216,31 @@ def test_blowfish_kat(brb, golden):
         brb.lib().BRB_Blowfish_Encrypt(ctypes.byref(c), ctypes.byref(xl), ctypes.byref(xr))
         got = (xl.value & 0xFFFFFFFF).to_bytes(4, "big") + (xr.value & 0xFFFFFFFF).to_bytes(4, "big")
         assert got.hex().upper() == v["cipher"]
+
+
+def test_md5_streaming_random_chunks(brb, orc):
+    """BRB_MD5Update and BRB_MD5UpdateBig interleaved over random chunk sizes (0..300 bytes, and
+    whole 64 KiB pieces) on 40 messages up to 200 KB: the context bytes equal the oracle's after every
+    call, and Final equals hashlib (md5.c:55-168)."""
+    rng = np.random.default_rng(77)
+    for m in range(40):
+        n = int(rng.integers(0, 200_000)) if m % 4 else int(rng.integers(0, 300))
+        data = workload.gen_records(0x5EED0C0C, m, 1, n).tobytes()
+        c = _md5_ctx(brb)
+        o = orc.Md5Ctx()
+        orc.lib().orc_md5_init(ctypes.byref(o))
+        pos = 0
+        while pos < n:
+            k = min(n - pos, 65536 if rng.random() < 0.05 else int(rng.integers(0, 301)))
+            piece = data[pos:pos + k]
+            if rng.random() < 0.5:
+                brb.lib().BRB_MD5Update(ctypes.byref(c), piece, k)
+                orc.lib().orc_md5_update(ctypes.byref(o), piece, k)
+            else:
+                brb.lib().BRB_MD5UpdateBig(ctypes.byref(c), piece, k)
+                orc.lib().orc_md5_update_big(ctypes.byref(o), piece, k)
+            assert bytes(c) == bytes(o), (m, pos, k)
+            pos += k
+        brb.lib().BRB_MD5Final(ctypes.byref(c))
+        orc.lib().orc_md5_final(ctypes.byref(o))
+        assert bytes(c.digest) == bytes(o.digest) == hashlib.md5(data).digest(), m
