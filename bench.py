@@ -36,7 +36,8 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s (device-resident) + Mrecords/s over 1500B buffers at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 TIMING = ("HIP events on the launch stream from the end of step 2 to the end of step K, / (K-2): back-to-back "
-          "launches without the first two after the idle synchronize (the wall time behind `value` includes them)")
+          "launches without the first two after the idle synchronize (the wall time behind `value` includes them); "
+          "launch_us_avg_all_k / frac_all_k: the same events over all K launches")
 L3_BYTES = 256 << 20
 SIMDS = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.1                # shader clock the chip holds with every CU issuing these kernels:
@@ -277,6 +278,7 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
 
 
 MARK = False     # --mark-timed-region
+LAST_ALL_K_S = None   # per-launch seconds of the last timed region over ALL K launches (events)
 
 
 def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
@@ -292,9 +294,13 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     20-step region under rocprofv3: 25.2 and 27.2 us, then 21.5-22.8 us).  Recording e0 after step
     2 rather than step 1 also keeps the host's event call off the critical path: enqueued between
     steps 1 and 2 it left a 5.6 us gap between the two kernels.  The wall time (and so `value`)
-    covers all K steps.  Nothing is enqueued between kernels.
+    covers all K steps.  Nothing is enqueued between kernels.  LAST_ALL_K_S keeps the same events'
+    time over all K launches (an event recorded before step 0), the round-2 method, so the two can be
+    compared.
     """
+    global LAST_ALL_K_S
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ea = torch.cuda.Event(enable_timing=True)
     if MARK:             # sentinel before the region, drained before t0
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
@@ -302,7 +308,9 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if not steady:
+    if steady:
+        ea.record(streams[0])
+    else:
         e0.record(streams[0])
     for k in range(n_steps):
         j = k % len(streams)
@@ -317,6 +325,7 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
             torch.cuda._sleep(1)
         torch.cuda.synchronize()
     wall = max_over_ranks(time.perf_counter() - t0)
+    LAST_ALL_K_S = ((ea if steady else e0).elapsed_time(e1) / 1e3 / n_steps) if len(streams) == 1 else None
     return wall, e0.elapsed_time(e1) / 1e3 / (n_steps - 2 if steady else n_steps)
 
 
@@ -390,6 +399,7 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
     n_warm, n_steps = warm_up(args, launch_raw, main_streams, torch, max_over_ranks)
     wall, ev_s = timed_steps(lambda k, s, j: launch_raw(k + n_warm, s, j), n_steps, main_streams,
                              barrier, max_over_ranks, torch)
+    all_k_s = LAST_ALL_K_S
     if cfg5 is not None:
         cfg5_verify()
     wall2 = None
@@ -439,6 +449,8 @@ def bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), **traffic_fields(args.pmc_summary, pmc_key),
                      "launch_us_avg": round(avg_kern_s * 1e6, 2), "bytes_per_launch": n_rank * L,
+                     "launch_us_avg_all_k": round(all_k_s * 1e6, 2) if all_k_s else None,
+                     "frac_all_k": round(n_rank * L / all_k_s / 1e9 / HBM_PEAK_GBS, 4) if all_k_s else None,
                      "timing": TIMING,
                      "compute": compute_fraction(args.pmc_summary, pmc_key, avg_kern_s,
                                                  LONE_WAVE_CYC.get(args.op) if n_rank <= 65536 else None)},

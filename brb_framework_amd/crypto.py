@@ -16,6 +16,7 @@ BATCH_DEVICE = 0x1
 BATCH_ASYNC = 0x2
 BATCH_ALL_DEVICES = 0x4
 BATCH_DROPPED = -2
+BATCH_PARTIAL = -3
 TRANSFORM_DROPPED = -1
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -159,12 +160,22 @@ def lib() -> ctypes.CDLL:
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in _SIGNATURES:
             f = getattr(L, name, None)
-            if f is None:        # an older build under A/B; tests/test_abi.py checks exports == header
+            if f is None:
+                # An older build (interleaved A/B runs load one): the library still loads, but the
+                # first call of a symbol it lacks raises here, naming it, instead of failing later
+                # with default ctypes argtypes.  tests/test_abi.py checks exports == header.
+                setattr(L, name, _missing_symbol(name))
                 continue
             f.restype = res
             f.argtypes = args
         _LIB = L
     return _LIB
+
+
+def _missing_symbol(name: str):
+    def call(*_a, **_k):
+        raise RuntimeError(f"{LIB_PATH} does not export {name} (a stale build?): rebuild with `make -C {HERE}`")
+    return call
 
 
 def exported_symbols() -> set:
@@ -601,17 +612,24 @@ class TransformBatcher:
         fn = TransformDone(cb)
         launched = self._used > 0
         rc = getattr(self._L, fn_name)(self.h, fn, None)
-        if rc == BATCH_DROPPED:
-            # every buffer came back through its callback; those of the dropped round with
-            # valid == TRANSFORM_DROPPED and no output
+        if rc in (BATCH_DROPPED, BATCH_PARTIAL):
+            # DROPPED: every buffer came back through its callback, those of the dropped round with
+            # valid == TRANSFORM_DROPPED and no output.  PARTIAL: the parts that delivered did; the
+            # others' rounds stay pending for the next flush.  Either way the delivered results ride
+            # on the exception.
             err = RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
             err.results = res
-            if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
-                self._cur ^= 1
-            self._used = 0
+            err.code = rc
+            if rc == BATCH_DROPPED:
+                if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
+                    self._cur ^= 1
+                self._used = 0
             raise err
         if rc < 0 or (rc == 0 and self._L.BRB_CryptoGPU_LastError()):
-            raise RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
+            err = RuntimeError(fn_name + ": " + self._L.BRB_CryptoGPU_LastError().decode())
+            err.results = res    # whatever callbacks fired before the failure
+            err.code = rc
+            raise err
         if fn_name.endswith("Async") and launched and self._regions is not None and len(self._regions) == 2:
             self._cur ^= 1      # the running round keeps its region until delivered
         self._used = 0

@@ -1008,7 +1008,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"var_line", brb_opt::kVarLine, 0, 1},
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
                  {"var_sort", brb_opt::kVarSort, 0, 2},
-                 {"devices", brb_opt::kDevices, 0, 64},
+                 {"devices", brb_opt::kDevices, 0, 16},   // an all-devices batcher takes at most 16 parts
                  {"b64_group", brb_opt::kB64Group, -1, 6}};
     if (!name) {
         set_err("NULL option name");

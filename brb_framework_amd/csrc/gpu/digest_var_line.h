@@ -84,13 +84,20 @@ constexpr uint32_t kSortNB = 8;       // buckets
 // The slice a group takes is rotated by its round t = g / gridDim.x: workgroup b owns groups
 // b + t gridDim.x, all with the same g mod kSortCG (gridDim.x is a multiple of it), so without the
 // rotation one workgroup in kSortCG took every chunk's longest slice in every round and set the
-// kernel time (measured: no gain at all on 524 288 records).  The kSortCG groups of one chunk share
-// t, so the rotation stays a bijection of the chunk's slices.
+// kernel time (measured: no gain at all on 524 288 records).  The groups of one chunk share t, so
+// the rotation is a bijection of the slices the chunk's groups take -- of all kSortCG in a whole
+// chunk, and of slices 0 .. pc-1 in a last chunk of pc < kSortCG groups: its records rank first
+// (a missing record is keyed into the last bucket, behind every real one of that bucket), so they
+// fill exactly slices 0 .. pc-1.  (Rotating over all kSortCG there sent a group to an empty slice
+// and left a slice of real records undigested)
 BRB_DEV uint64_t sorted_record(uint64_t g, uint32_t lane, const uint32_t *__restrict__ lens, uint64_t n_rec,
                                uint32_t *scratch)
 {
-    const uint64_t c0 = (g / kSortCG) * kSortCG * 64;
-    const uint32_t j = uint32_t((g % kSortCG + g / gridDim.x) % kSortCG);
+    const uint64_t cg = (g / kSortCG) * kSortCG;              // the chunk's first group
+    const uint64_t c0 = cg * 64;
+    const uint64_t left = (n_rec + 63) / 64 - cg;             // groups of this chunk (>= 1)
+    const uint32_t pc = left < kSortCG ? uint32_t(left) : kSortCG;
+    const uint32_t j = uint32_t((g % kSortCG + g / gridDim.x) % pc);
     uint32_t it[kSortCG];
     bool ok[kSortCG];
     uint32_t lo = 0xFFFFFFFFu, hi = 0;

@@ -282,7 +282,9 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
         algo &= ~BRB_BATCHER_ALL_DEVICES;
         if (brb_api::device_ok() != BRB_BATCH_OK)
             return nullptr;
-        const int G = brb_host::split_parts();
+        // at most kChunks parts: a thread keeps one chunk entry per part's round (with
+        // more parts than entries every round-robin submit evicted a live chunk)
+        const int G = std::min(brb_host::split_parts(), kChunks);
         if (G > 1 && max_conns >= uint32_t(G)) {
             auto *m = new BRB_TransformBatcher;
             m->max_conns = max_conns;
@@ -712,6 +714,11 @@ static void phase_deliver(Phase &p, Round &R)
     if (!R.in_flight)
         return;
     DeviceGuard g(p.b->dev);
+    if (g.error() != hipSuccess) {      // the round stays in flight: a later Flush delivers it
+        fail_hip("hipSetDevice", g.error());
+        p.failed = true;
+        return;
+    }
     const int64_t n = deliver_round(p.b, R, p.done, p.user);
     if (n < 0)
         p.dropped = true;
@@ -768,13 +775,26 @@ static int64_t flush_all(BRB_TransformBatcher *b, BRB_TransformDone done, void *
                 phase_deliver(p, *p.prev);
     }
     int64_t total = 0;
-    bool dropped = false, failed = false;
+    bool dropped = false;
+    uint32_t failed = 0;
     for (const Phase &p : ph) {
         total += p.n;
         dropped |= p.dropped;
-        failed |= p.failed;
+        failed += p.failed ? 1u : 0u;
     }
-    return dropped ? BRB_BATCH_DROPPED : failed ? BRB_BATCH_NOT_DONE : total;
+    if (dropped)
+        return BRB_BATCH_DROPPED;
+    if (failed) {
+        // parts that could not select their device keep their rounds pending, while the
+        // other parts' buffers were delivered (callbacks fired, states advanced): say so instead of
+        // returning "not done" for the whole call
+        const std::string why = brb_api::t_err;
+        set_err("%u of %u parts could not select their device (%s); their rounds stay pending, %lld buffers of "
+                "the other parts were delivered; Flush again",
+                failed, G, why.c_str(), (long long)total);
+        return total ? BRB_BATCH_PARTIAL : BRB_BATCH_NOT_DONE;
+    }
+    return total;
 }
 
 extern "C" {

@@ -110,6 +110,9 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
 #define BRB_BATCH_NOT_DONE  0
 #define BRB_BATCH_BADARG   (-1)
 #define BRB_BATCH_DROPPED  (-2)   /* transform batcher: a round was dropped (see Flush)         */
+#define BRB_BATCH_PARTIAL  (-3)   /* all-devices transform batcher: some parts delivered their
+                                     buffers, others could not select their device and keep their
+                                     rounds pending (see Flush)                                  */
 
 /* flags */
 #define BRB_BATCH_HOST      0x0u   /* pointers are host memory: copied in and out by the call      */
@@ -129,7 +132,13 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
 
 /* Device mode: `hip_stream` is a hipStream_t (NULL = the legacy default stream of the current
  * device) and the work runs on the caller's current HIP device (BRB_CryptoGPU_SetDevice,
- * hipSetDevice or torch.cuda.set_device).  Host mode: the call runs on the caller's current device
+ * hipSetDevice or torch.cuda.set_device).
+ * DEVICE-MODE CONTRACT: the library cannot see how large a device allocation is, so in device mode
+ * every offset, length and count is the caller's promise that the range lies inside its allocation
+ * (data, offsets/lengths arrays, digests, outputs, states).  A range past the end is not detected
+ * and not answered with -1: the kernel's access faults and the HIP context is lost ("illegal memory
+ * access", every later call on that device fails).  Host mode copies exactly the ranges given, so
+ * there a bad range is an ordinary out-of-bounds read of the caller's host memory.  Host mode: the call runs on the caller's current device
  * (or on every device with BRB_BATCH_ALL_DEVICES), copies straight from and to the caller's memory
  * (pageable or page-locked) in chunks so that copies in both directions overlap the kernels, and
  * returns when the results are in host memory; `hip_stream` is not used. */
@@ -283,7 +292,11 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
  * chunks, so a round shared by T threads may report full up to T chunks (64 buffers, 128 KiB) early. */
 int BRB_TransformBatcherRead(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len);
 int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void *data, uint32_t len, uint64_t salt);
-/* Runs the round; returns the number of buffers delivered, or -1 for bad arguments.  A round that
+/* Runs the round; returns the number of buffers delivered, or -1 for bad arguments.  All-devices
+ * batcher: a part that cannot select its device (hipSetDevice fails) keeps its round pending and
+ * delivers nothing, while the other parts deliver as usual; the call then returns
+ * BRB_BATCH_PARTIAL (-3) if some buffers were delivered, 0 if none, with the parts and the
+ * delivered count in LastError -- Flush again once the device is back.  A round that
  * fails on the device is dropped and never re-run (kernels launched before the failure may have
  * advanced their connections' states; running them again would advance them twice): each of its
  * buffers still gets its callback, in order, with valid = BRB_TRANSFORM_DROPPED, out = NULL and
@@ -372,8 +385,8 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * (variable-length digests on the line kernel / on the per-lane kernel), "fixed_var_line" 1/0
  * (unaligned fixed-stride records on the line kernel / record-relative kernel), "var_sort" 1/0
  * (variable-length batches bucketed by length / in caller order; 2 keeps the first round of groups in
- * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k parts,
- * part g on device g % count), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
+ * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k <= 16
+ * parts, part g on device g % count; an all-devices batcher takes at most 16 parts either way), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
  * forced to 2^value).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);

@@ -150,3 +150,27 @@ def test_multi_device_runtime_without_gpu(brb):
     data = np.zeros(64 * 4, np.uint8)
     with pytest.raises(RuntimeError, match="returned 0"):
         brb.md5_batch_fixed(data, 64, all_devices=True)
+
+
+def test_test_option_ranges(brb):
+    """BRB_CryptoGPU_TestOption refuses unknown names and values out of range (no device needed).
+    "devices" stops at 16: an all-devices batcher's submitting threads keep one chunk entry per
+    part's round, 16 of them."""
+    old = ctypes.c_int(0)
+    L = brb.lib()
+    assert L.BRB_CryptoGPU_TestOption(b"devices", 17, ctypes.byref(old)) == -1
+    assert b"out of" in L.BRB_CryptoGPU_LastError()
+    assert L.BRB_CryptoGPU_TestOption(b"no_such_option", 0, None) == -1
+    with brb.TestOption("devices", 16):
+        pass
+    with brb.TestOption("var_sort", 2):
+        pass
+
+
+def test_missing_symbol_raises_by_name(brb, monkeypatch):
+    """A stale library that lacks a header symbol still loads (A/B runs of older builds), but a call
+    of that symbol raises at once, naming it (no silent default argtypes)."""
+    from brb_framework_amd import crypto
+    stub = crypto._missing_symbol("BRB_NoSuchCall")
+    with pytest.raises(RuntimeError, match="BRB_NoSuchCall"):
+        stub(1, 2)

@@ -63,8 +63,9 @@ def test_timed_steps_covers_launches_3_to_k():
 
     bench.MARK = False
     wall, per = bench.timed_steps(launch, 5, ["s0"], lambda: None, lambda x: x, torch)
-    assert clock.log == ["launch0", "launch1", "event", "launch2", "launch3", "launch4", "event"]
+    assert clock.log == ["event", "launch0", "launch1", "event", "launch2", "launch3", "launch4", "event"]
     assert abs(per - 2.0e-3) < 1e-12          # seconds per launch
+    assert abs(bench.LAST_ALL_K_S - (5 * 2.0 + 70.0) / 5 / 1e3) < 1e-12   # all K, the stalls included
     assert wall >= 0
 
 

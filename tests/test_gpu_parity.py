@@ -451,6 +451,30 @@ def test_variable_records_bucketed(brb, orc, torch_dev, n, kind, sort):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sort", [1, 2])
+@pytest.mark.parametrize("pc,short", [(1, 0), (2, 5), (3, 0), (3, 63)])
+def test_variable_records_bucketed_partial_chunk(brb, orc, torch_dev, pc, short, sort):
+    """the last chunk of a bucketed batch holds pc < 4 groups and its round
+    t = g / CUs is not a multiple of 4.  The slice rotation must stay inside the pc slices that
+    hold records (the round-3 kernel rotated over all 4, so a group took an empty slice and 64
+    records were never digested).  n = 64 (9 CUs + pc) - short puts the last chunk at round 9 on
+    any CU count; every digest is checked against the oracle, with var_sort 1 and 2."""
+    cus = torch_dev.cuda.get_device_properties(0).multi_processor_count
+    n = 64 * (9 * cus + pc) - short
+    rng = np.random.default_rng(1000 * pc + short)
+    lens = rng.integers(100, 700, n).astype(np.uint32)
+    offs = (np.cumsum(lens.astype(np.uint64)) - lens).astype(np.uint64)
+    buf = workload.gen_records(0x5EED0015, n, 1, int(lens.astype(np.uint64).sum()) + 64)
+    want = orc.md5_batch(buf, offs, lens, threads=16)
+    d, o, ln = to_dev(torch_dev, buf), to_dev(torch_dev, offs.view(np.int64)), to_dev(torch_dev, lens.view(np.int32))
+    with brb.TestOption("var_sort", sort):
+        got = brb.md5_batch(d, o, ln).cpu().numpy()
+        bad = np.nonzero(~np.all(got == want, axis=1))[0]
+        assert bad.size == 0, f"{bad.size} digests differ, first at record {bad[:4]} of {n}"
+        assert np.array_equal(brb.sha1_batch(d, o, ln).cpu().numpy(), orc.sha1_batch(buf, offs, lens, threads=16))
+
+
+@pytest.mark.gpu
 def test_variable_records_wide_span(brb, orc, torch_dev):
     """Groups whose records lie more than 2 GiB apart (32-bit DMA offsets cannot reach them) are
     digested by the per-lane path inside the same launch; the other groups stay line-staged."""
