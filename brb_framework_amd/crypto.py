@@ -8,7 +8,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbrb_crypto_gpu.so")
+# BRB_CRYPTO_LIB: another build of the same library for the test plumbing (the ASan/UBSan build of
+# tools/sanitize_check.sh); the C library itself reads no environment variable.
+LIB_PATH = os.environ.get("BRB_CRYPTO_LIB") or os.path.join(HERE, "libbrb_crypto_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "brb_crypto.h")
 
 BATCH_HOST = 0x0

@@ -1009,7 +1009,9 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"fixed_var_line", brb_opt::kFixedVarLine, 0, 1},
                  {"var_sort", brb_opt::kVarSort, 0, 2},
                  {"devices", brb_opt::kDevices, 0, 16},   // an all-devices batcher takes at most 16 parts
-                 {"b64_group", brb_opt::kB64Group, -1, 6}};
+                 {"b64_group", brb_opt::kB64Group, -1, 6},
+                 {"host_chunk_mib", brb_opt::kHostChunkMiB, 0, 1024},
+                 {"host_digest_chunk_mib", brb_opt::kHostDigestChunkMiB, 0, 1024}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

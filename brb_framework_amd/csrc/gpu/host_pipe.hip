@@ -33,26 +33,21 @@ using brb_api::set_err;
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Input bytes per chunk (read once; BRB_HOST_CHUNK_BYTES / BRB_HOST_DIGEST_CHUNK_BYTES override).
-// Every pageable chunk copy pays a fixed cost (8 MiB pieces copy at 52 GB/s, one 98 MB copy at
-// 56.5 GB/s), while only the first chunk's H2D and the last chunk's D2H go un-overlapped.
-// Blowfish returns as many bytes as it sends, so its ends are whole chunks: 16 MiB.  Digest
-// batches return 16-20 B per record, so their chunks can be larger: 32 MiB.
-size_t env_bytes(const char *name, size_t dflt)
-{
-    const char *e = getenv(name);
-    const long long x = e ? atoll(e) : 0;
-    return x >= 4096 ? size_t(x) : dflt;
-}
+// Input bytes per chunk.  Every pageable chunk copy pays a fixed cost (8 MiB pieces copy at
+// 52 GB/s, one 98 MB copy at 56.5 GB/s), while only the first chunk's H2D and the last chunk's D2H
+// go un-overlapped.  Blowfish returns as many bytes as it sends, so its ends are whole chunks:
+// 16 MiB.  Digest batches return 16-20 B per record, so their chunks can be larger: 32 MiB.
+// Test options "host_chunk_mib" / "host_digest_chunk_mib" (0 = these defaults) change them for
+// sweeps (tools/host_sweep.py); the library reads no environment variable.
 size_t chunk_bytes()
 {
-    static const size_t v = env_bytes("BRB_HOST_CHUNK_BYTES", size_t(16) << 20);
-    return v;
+    const int mib = brb_opt::get(brb_opt::kHostChunkMiB);
+    return (mib > 0 ? size_t(mib) : size_t(16)) << 20;
 }
 size_t digest_chunk_bytes()
 {
-    static const size_t v = env_bytes("BRB_HOST_DIGEST_CHUNK_BYTES", size_t(32) << 20);
-    return v;
+    const int mib = brb_opt::get(brb_opt::kHostDigestChunkMiB);
+    return (mib > 0 ? size_t(mib) : size_t(32)) << 20;
 }
 
 // Posts "wait for `ev` on `s_out`, then copy [src, src + bytes) to host `dst`" to the device's D2H

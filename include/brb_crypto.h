@@ -387,7 +387,8 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * (variable-length batches bucketed by length / in caller order; 2 keeps the first round of groups in
  * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k <= 16
  * parts, part g on device g % count; an all-devices batcher takes at most 16 parts either way), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
- * forced to 2^value).  Returns 1 and the previous
+ * forced to 2^value), "host_chunk_mib" / "host_digest_chunk_mib" 0/k (host-mode chunks of the default
+ * 16 / 32 MiB, or k MiB; chunk-size sweeps).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("BRB_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")   # sanitizer builds
 
 _L = None
 u64 = ctypes.c_uint64

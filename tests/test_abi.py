@@ -11,7 +11,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "include", "brb_crypto.h")
-LIBDIR = os.path.join(ROOT, "brb_framework_amd")
+LIBDIR = os.path.dirname(os.environ.get("BRB_CRYPTO_LIB") or os.path.join(ROOT, "brb_framework_amd", "x"))
 
 
 def header_functions():

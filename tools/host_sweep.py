@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Host-mode (PCIe-inclusive) rates vs chunk size: for each setting a fresh process
-(the chunk sizes are read once per process) times cfg2 and cfg3 digests and the cfg4 Blowfish round
+(chunk sizes set through the test options host_digest_chunk_mib / host_chunk_mib) times cfg2 and cfg3 digests and the cfg4 Blowfish round
 trip from pageable and page-locked host memory.
 
 Usage: python tools/host_sweep.py [digest_chunk_MiB,blowfish_chunk_MiB ...]   (default: 32,16)"""
@@ -29,7 +29,10 @@ def child():
         dt = (time.perf_counter() - t) / reps
         return round(nbytes / dt / 1e9, 2)
 
-    res = {"digest_chunk": os.environ.get("BRB_HOST_DIGEST_CHUNK_BYTES"), "chunk": os.environ.get("BRB_HOST_CHUNK_BYTES")}
+    d_mib, b_mib = (int(x) for x in os.environ["HOST_SWEEP_CHILD"].split(","))
+    brb.test_option("host_digest_chunk_mib", d_mib)
+    brb.test_option("host_chunk_mib", b_mib)
+    res = {"digest_chunk_mib": d_mib, "chunk_mib": b_mib}
     for c in (2, 3):
         cfg = workload.CONFIGS[c]
         n, L = cfg["records"], cfg["rec_len"]
@@ -58,8 +61,7 @@ def main():
     settings = sys.argv[1:] or ["32,16"]
     for st in settings:
         d, b = (int(x) for x in st.split(","))
-        env = dict(os.environ, HOST_SWEEP_CHILD="1", BRB_HOST_DIGEST_CHUNK_BYTES=str(d << 20),
-                   BRB_HOST_CHUNK_BYTES=str(b << 20))
+        env = dict(os.environ, HOST_SWEEP_CHILD=f"{d},{b}")
         subprocess.run([sys.executable, __file__], env=env, check=True, timeout=300)
 
 
