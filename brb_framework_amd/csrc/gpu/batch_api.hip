@@ -1011,7 +1011,8 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"devices", brb_opt::kDevices, 0, 16},   // an all-devices batcher takes at most 16 parts
                  {"b64_group", brb_opt::kB64Group, -1, 6},
                  {"host_chunk_mib", brb_opt::kHostChunkMiB, 0, 1024},
-                 {"host_digest_chunk_mib", brb_opt::kHostDigestChunkMiB, 0, 1024}};
+                 {"host_digest_chunk_mib", brb_opt::kHostDigestChunkMiB, 0, 1024},
+                 {"seg_line", brb_opt::kSegLine, 0, 1}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -1,0 +1,186 @@
+// line_stream.h -- per-lane byte streams staged through the line-aligned LDS-DMA ring, for the
+// MD5 kernels whose message is a lane's own sequence of byte ranges: the segment lists of
+// BRB_MD5BatchSegments (md5_seg_kernels.hip) and the item data of MetaData packs
+// (metadata_kernels.hip; meta_data.c:145-290, 397-433).
+//
+// The fixed-stride and variable-length digests (digest_line.h, digest_var_line.h) stage a lane's
+// record as 128-byte memory lines, 64 rows (one per lane) x one line per ring slot, by LDS-DMA
+// (buffer_load_dwordx4 ... lds): no VGPRs in flight, whole lines requested once, the next line
+// landing while the lane hashes the previous one.  Here a lane's lines form a VIRTUAL line sequence
+// -- its segments' lines one after another (a segment's lines are contiguous in memory; the next
+// segment's first line may be anywhere) -- so every stage gathers each row's next line offset
+// from its lane (8 ds_bpermute) instead of advancing one shared descriptor.  The descriptor's base
+// is 4 KiB below the group's lowest line; a group whose lines span 2 GiB or more (32-bit voffsets)
+// takes the per-lane block path instead.
+//
+// Consumption: iteration k reads the 33-dword window of lines k-1 and k (slots (k-1) & 1, k & 1)
+// and EMITS the message words of the lane's current range that start in line k-1, into the lane's
+// 64-word funnel ring (md5_funnel.h FunnelT<64>); whole 16-word blocks are then compressed from the
+// ring.  A range is read on a word grid that starts e = (message bytes before it) mod 4 bytes
+// before the range (as the per-lane kernels do), so message words are one v_alignbit of two window
+// dwords each and the first word's low e bytes are the carried ones (Funnel::head).  A word is
+// emitted in the line that holds its first byte (a range's first word: in the line that holds the
+// range's first byte), so at most 33 words leave one line, and a word that runs into line k reads
+// it from the window (line k is the next line of the same range whenever a range continues).
+#pragma once
+
+#include "digest_line.h"
+#include "md5_funnel.h"
+
+namespace brb_line {
+
+constexpr uint32_t kSlot = 8192;          // one ring slot: 64 rows x one 128-byte line
+constexpr uint32_t kOOB = 0x80000000u;    // a voffset past every descriptor's range (DMA returns 0)
+constexpr uint32_t kRingWords = 64;       // funnel ring words per lane
+
+// LDS addresses of window dword j (0..32) of this lane for the window (k-1, k) with line k-1 in
+// slot 0 (ae) or slot 1 (ao).  Row `lane` of slot s holds the lane's line at granule positions
+// swizzled by swz(row) = (row >> 1) & 7 (applied on the DMA source side), so all 64 lanes reading
+// the same window dword hit different banks.
+struct Win {
+    uint32_t ae[33], ao[33];
+    BRB_DEV void init(uint32_t slot0_lds, uint32_t lane)
+    {
+        const uint32_t fr = (slot0_lds + lane * 128) | (((lane >> 1) & 7) << 4);
+#pragma unroll
+        for (uint32_t j = 0; j < 33; j++) {
+            const uint32_t q4 = 4 * j;
+            ae[j] = ((q4 & 124u) ^ fr) + ((q4 & 128u) << 6);
+            ao[j] = ae[j] ^ kSlot;
+            asm volatile("" : "+v"(ao[j]));     // keep both tables (hipcc re-derived ao per use)
+        }
+    }
+};
+
+BRB_DEV uint32_t lds_ld(uint32_t a) { return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(a); }
+
+// The 33 window dwords; returns once they are in registers (lgkmcnt(0)), so the slot of line k-1
+// may be refilled right after.
+BRB_DEV void read_window(const uint32_t (&ad)[33], uint32_t (&dw)[33])
+{
+#pragma unroll
+    for (int j = 0; j < 33; j++)
+        dw[j] = lds_ld(ad[j]);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+}
+
+// Stage one line per row into the slot at LDS address `lm`: row r's line is `rel` of lane r
+// (its offset from the group's lowest line, a multiple of 128), or kOOB for none.  DMA lane
+// (q, l3 = lane >> 3) moves granule (lane & 7) ^ swz(row) of row 8q + l3's line; the descriptor's
+// base is 4 KiB below the lowest line and four DMAs share one M0 through their instruction offsets.
+BRB_DEV void issue_rows(const brb_dma::v4i &rs, uint32_t lm, uint32_t rel, uint32_t lane)
+{
+    const uint32_t l3 = lane >> 3;
+    const uint32_t g0 = 16u * ((lane & 7) ^ (l3 >> 1));   // swz(8q + l3) = (l3 >> 1) ^ 4 (q & 1)
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const uint32_t rr = uint32_t(__builtin_amdgcn_ds_bpermute(int(8 * q + l3) * 4, int(rel)));
+        v[q] = rr >= kOOB ? kOOB : (rr | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
+    }
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\t"
+                 "s_mov_b32 m0, %10\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %1, %9, 0 offen nt lds\n\t"
+                 "buffer_load_dwordx4 %2, %9, 0 offen offset:1024 nt lds\n\t"
+                 "buffer_load_dwordx4 %3, %9, 0 offen offset:2048 nt lds\n\t"
+                 "buffer_load_dwordx4 %4, %9, 0 offen offset:3072 nt lds\n\t"
+                 "s_mov_b32 m0, %11\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %5, %9, 0 offen nt lds\n\t"
+                 "buffer_load_dwordx4 %6, %9, 0 offen offset:1024 nt lds\n\t"
+                 "buffer_load_dwordx4 %7, %9, 0 offen offset:2048 nt lds\n\t"
+                 "buffer_load_dwordx4 %8, %9, 0 offen offset:3072 nt lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+                   "s"(rs), "s"(lm), "s"(lm + 4096u)
+                 : "memory");
+}
+
+// Descriptor for a group whose lines lie in [lo, hi) (128-byte aligned absolute addresses).
+BRB_DEV brb_dma::v4i group_rsrc(uint64_t lo, uint64_t hi)
+{
+    const uint64_t base = lo - 4096;
+    const uint64_t left = hi - base;
+    brb_dma::v4i r;
+    r.x = __builtin_amdgcn_readfirstlane(int(uint32_t(base)));
+    r.y = __builtin_amdgcn_readfirstlane(int(uint32_t(base >> 32) & 0xFFFF));
+    r.z = __builtin_amdgcn_readfirstlane(int(left > 0x7FFFFFFFull ? 0x7FFFFFFFu : uint32_t(left)));
+    r.w = 0x00020000;
+    return r;
+}
+
+// The range a staged line belongs to, in offsets from the group's lowest line: the line itself, the
+// range's first byte and its end.  line == kOOB: the lane has no line in this slot.
+struct LineDesc {
+    uint32_t line, ss, se;
+};
+
+// Emits the message words of one range that start in the window's line k-1 (see the file comment).
+//   d      the line and its range (d.line != kOOB)
+//   b      the lane's word-grid phase inside lines (0..3), set at the range's first line
+//   dw     the 33 window dwords
+// Whole words go to the funnel ring; if the range ends in this line, the bytes of its last partial
+// word become the carry.  Returns nothing; f.wpos / acc / nacc / total advance.
+template <uint32_t RW>
+BRB_DEV void emit_range(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[33])
+{
+    const bool first = d.ss >= d.line;                        // the range starts in this line
+    int o;                                                    // grid offset of the first word (-3..127)
+    uint32_t e = 0;
+    if (first) {
+        e = f.nacc;
+        o = int(d.ss - d.line) - int(e);
+        b = uint32_t(o) & 3u;
+        f.total += d.se - d.ss;
+    } else {
+        o = int(b);
+    }
+    const uint32_t endr = d.se - d.line < 4096u ? d.se - d.line : 4096u;   // range end, line-relative
+    if (int(endr) <= o)                                       // its last word started in the line before
+        return;
+    const int i0 = o >> 2;                                    // -1 .. 31
+    const int span = int(endr) - int(b);                      // > 4 i0
+    const int iw = span >> 2 < 32 ? span >> 2 : 32;           // whole words: i0 <= i < iw
+    const bool ends = span <= 128;                            // the range's last word starts here
+    const uint32_t rem = uint32_t(span) & 3u;                 // bytes of a last partial word
+    const int it = span >> 2;                                 // its index (when ends && rem)
+    const uint32_t sh = 8 * b;
+    const uint32_t carry = uint32_t(f.acc);
+    const uint32_t hmask = e ? (1u << (8 * e)) - 1u : 0u;
+    // word i goes to ring position wpos + i - i0
+    const uint32_t wbase = f.lane4 + ((f.wpos - uint32_t(i0)) << 8);
+    uint32_t tail = 0;
+#pragma unroll
+    for (int i = -1; i < 32; i++) {
+        uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], sh);
+        if (i == i0)
+            v = (v & ~hmask) | (carry & hmask);               // Funnel::head on the range's first word
+        if (i >= i0 && i < iw)
+            brb_md5::FunnelT<RW>::lds_st(((wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring, v);
+        tail = i == it ? v : tail;
+    }
+    f.wpos += uint32_t(iw > i0 ? iw - i0 : 0);
+    if (ends) {
+        f.nacc = rem;
+        f.acc = rem ? (tail & ((1u << (8 * rem)) - 1u)) : 0u;
+    }
+}
+
+// All 32 words of a line that lies wholly inside the lane's current range, not its first line
+// (the common case): no head, no bounds, no tail.
+template <uint32_t RW>
+BRB_DEV void emit_whole_line(brb_md5::FunnelT<RW> &f, uint32_t b, const uint32_t (&dw)[33])
+{
+    const uint32_t sh = 8 * b;
+    const uint32_t wbase = f.lane4 + (f.wpos << 8);
+#pragma unroll
+    for (int i = 0; i < 32; i++)
+        brb_md5::FunnelT<RW>::lds_st(((wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring,
+                                     __builtin_amdgcn_alignbit(dw[i + 1], dw[i], sh));
+    f.wpos += 32;
+}
+
+}  // namespace brb_line

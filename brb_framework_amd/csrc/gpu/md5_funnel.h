@@ -17,9 +17,14 @@ namespace brb_md5 {
 
 constexpr uint32_t kRingWords = 32;
 
-struct Funnel {
+// RW ring words per lane (a multiple of 16, a power of two): the wave's ring is RW x 64 dwords at an
+// RW * 256-byte aligned LDS address.  The line-staged kernels (line_stream.h) put up to 33 words per
+// 128-byte line and take RW = 64; the per-lane block kernels put 16 per block and take 32.
+template <uint32_t RW>
+struct FunnelT {
+    static constexpr uint32_t kMask = RW * 256 - 1;
     uint32_t *bb;       // ring word k of this lane at bb[64 k] (LDS)
-    uint32_t ring;      // LDS address of this wave's ring (8 KiB aligned), OR'd into word addresses
+    uint32_t ring;      // LDS address of this wave's ring (RW * 256-byte aligned), OR'd into word addresses
     uint32_t lane4;     // 4 x lane: the lane's byte within a ring row
     Md5State st;
     uint64_t acc, total; // the carried bytes (low nacc bytes), message bytes so far (the caller's)
@@ -27,13 +32,13 @@ struct Funnel {
     uint32_t wpos;      // words written
     uint32_t cpos;      // words compressed (a multiple of 16)
 
-    // lane_words = &ring[0][lane] of a [32][64] uint32 array at an 8 KiB-aligned LDS address (the
-    // kernels' only __shared__ array), so a word's address is one and-or of its ring offset
+    // lane_words = &ring[0][lane] of a [RW][64] uint32 array at an RW * 256-byte aligned LDS
+    // address, so a word's address is one and-or of its ring offset
     BRB_DEV void init(uint32_t *lane_words)
     {
         bb = lane_words;
         const uint32_t a = uint32_t(reinterpret_cast<uintptr_t>(lane_words));
-        ring = a & ~0x1FFFu;
+        ring = a & ~kMask;
         lane4 = a & 0xFFu;
         st = md5_iv();
         acc = total = 0;
@@ -42,10 +47,10 @@ struct Funnel {
 
     static BRB_DEV void lds_st(uint32_t a, uint32_t v) { *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(a) = v; }
 
-    // word at ring position wpos + i (mod 32): (lane4 + 256 (wpos + i)) mod 8 KiB, in the wave's ring
+    // word at ring position wpos + i (mod RW): (lane4 + 256 (wpos + i)) mod (RW * 256), in the wave's ring
     BRB_DEV void word_at(uint32_t i, uint32_t w) const
     {
-        lds_st(((lane4 + ((wpos + i) << 8)) & 0x1FFFu) | ring, w);
+        lds_st(((lane4 + ((wpos + i) << 8)) & kMask) | ring, w);
     }
     BRB_DEV void word(uint32_t w)
     {
@@ -87,7 +92,7 @@ struct Funnel {
     // cpos is a multiple of 16, so the 16 words never wrap: one base, immediate offsets
     BRB_DEV void load16(uint32_t (&w)[16]) const
     {
-        const uint32_t *b = bb + 64 * (cpos & 16);
+        const uint32_t *b = bb + 64 * (cpos & (RW - 16));
 #pragma unroll
         for (uint32_t i = 0; i < 16; i++)
             w[i] = b[64 * i];
@@ -126,5 +131,7 @@ struct Funnel {
         return st;
     }
 };
+
+using Funnel = FunnelT<kRingWords>;
 
 }  // namespace brb_md5

@@ -8,33 +8,26 @@
 // funnelled into the lane's MD5 (md5_funnel.h).
 #include "brb_kernels.h"
 #include "byte_stream.h"
+#include "digest_var_line.h"
+#include "line_stream.h"
 #include "md5_funnel.h"
+#include "test_options.h"
 
 namespace {
 
 constexpr int kBlock = 256;
 
-__global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restrict__ data,
-                                                         const uint64_t *__restrict__ soff,
-                                                         const uint32_t *__restrict__ slen,
-                                                         const uint64_t *__restrict__ first, uint64_t n_rec,
-                                                         uint8_t *__restrict__ out)
+// The per-lane block path: record r's segments read in 64-byte blocks (brb_io::BlockSrc, the next
+// block in flight, the next segment's first block in flight while the current one is hashed) and
+// funnelled into the lane's MD5.  Segment k is read as a range starting e_k = (bytes before it)
+// mod 4 bytes before it, so its words fall on the digest's word boundaries (Funnel::head); those e
+// bytes are the carried ones, never loaded from below the segment.  Used for groups whose lines span
+// 2 GiB or more, and by the round-3 kernel kept for A/B (test option seg_line = 0).
+template <uint32_t RW>
+BRB_DEV void seg_lane(brb_md5::FunnelT<RW> &f, const uint8_t *__restrict__ data, const uint64_t *__restrict__ soff,
+                      const uint32_t *__restrict__ slen, uint64_t k, uint64_t k1)
 {
-    __shared__ __attribute__((aligned(8192))) uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];   // 8 KiB per wave
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n_rec)
-        return;
-    brb_md5::Funnel f;
-    f.init(&blk[wave][0][lane]);
-    const uint64_t k1 = first[r + 1];
-    // Segment k is read as a range starting e_k = (bytes before it) mod 4 bytes before it, so its
-    // words fall on the digest's word boundaries (as metadata_unpack_kernel): those e bytes are the
-    // carried ones (Funnel::head), never loaded from below the segment.  e_k depends only on the
-    // lengths, so segment k + 1's source starts (its first block in flight) before segment k is
-    // hashed: the two sources alternate (sa, sb: no register copies), and a segment's first block no
-    // longer waits a whole HBM round trip after the previous segment's last one.
-    uint64_t k = first[r], before = 0;
+    uint64_t before = 0;
     auto skip_empty = [&](uint64_t kk) {                // the next segment with bytes (an empty one's
         while (kk < k1 && slen[kk] == 0)                // address need not be memory)
             kk++;
@@ -86,9 +79,165 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
         run(sb, lb);
         before += lb;
     }
-    const Md5State st = f.finish();
+}
+
+BRB_DEV void store_digest(uint8_t *out, uint64_t r, const Md5State &st)
+{
     const uint4 v = make_uint4(st.a, st.b, st.c, st.d);
     __builtin_memcpy(out + 16 * r, &v, 16);
+}
+
+// Round-3 kernel (one record per lane, per-lane block loads), kept for A/B runs.
+__global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restrict__ data,
+                                                         const uint64_t *__restrict__ soff,
+                                                         const uint32_t *__restrict__ slen,
+                                                         const uint64_t *__restrict__ first, uint64_t n_rec,
+                                                         uint8_t *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(8192))) uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];   // 8 KiB per wave
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (r >= n_rec)
+        return;
+    brb_md5::Funnel f;
+    f.init(&blk[wave][0][lane]);
+    seg_lane(f, data, soff, slen, first[r], first[r + 1]);
+    store_digest(out, r, f.finish());
+}
+
+// Line-staged kernel (round 4; line_stream.h).  A wave digests groups of 64 records, one per lane;
+// a lane's VIRTUAL lines are its non-empty segments' 128-byte memory lines in order, staged two
+// ahead by LDS-DMA into a two-slot ring.  Per line: the 33-dword window, the next stage issued, the
+// segment's words that start in this line emitted into the lane's 64-word funnel ring, and up to
+// three 16-word blocks compressed.  W waves per workgroup, W * 32 KiB of LDS; groups strided over
+// the grid.
+template <int W>
+__global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__restrict__ data,
+                                                               const uint64_t *__restrict__ soff,
+                                                               const uint32_t *__restrict__ slen,
+                                                               const uint64_t *__restrict__ first, uint64_t n_rec,
+                                                               uint8_t *__restrict__ out)
+{
+    using namespace brb_line;
+    constexpr uint32_t RW = brb_line::kRingWords;
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * 2 * kSlot];
+    __shared__ __attribute__((aligned(16384))) uint32_t fring[W][RW][64];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * 2 * kSlot;
+    const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    Win win;
+    win.init(lds0, lane);
+
+    for (uint64_t g = uint64_t(blockIdx.x) * W + wv; g < n_groups; g += uint64_t(gridDim.x) * W) {
+        const uint64_t rec = g * 64 + lane;
+        const bool valid = rec < n_rec;
+        const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
+        // the group's line span and every lane's line count
+        uint64_t lo = ~uint64_t(0), hi = 0;
+        uint32_t nl = 0;
+        for (uint64_t kk = k0; kk < k1; kk++) {
+            const uint32_t len = slen[kk];
+            if (!len)
+                continue;
+            const uint64_t a = dbase + soff[kk];
+            const uint64_t l0 = a & ~uint64_t(127), l1 = (a + len + 127) & ~uint64_t(127);
+            lo = l0 < lo ? l0 : lo;
+            hi = l1 > hi ? l1 : hi;
+            nl += uint32_t((l1 - l0) >> 7);
+        }
+        lo = brb_digest::uniform64(brb_digest::wave_min64(lo));
+        hi = brb_digest::uniform64(brb_digest::wave_max64(hi));
+        const uint32_t K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
+        brb_md5::FunnelT<RW> f;
+        f.init(&fring[wv][0][lane]);
+        if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {   // no line, or too wide
+            if (valid) {
+                seg_lane(f, data, soff, slen, k0, k1);
+                store_digest(out, rec, f.finish());
+            }
+            continue;
+        }
+        const brb_dma::v4i rs = group_rsrc(lo, hi);      // K >= 1 here (some lane has a line)
+
+        // stage cursor: the next line to stage (offset from lo) and the segment it belongs to
+        uint32_t c_line = kOOB, c_last = 0, c_ss = 0, c_se = 0;
+        uint64_t nk = k0;                               // the next candidate segment, prefetched
+        uint32_t n_len = 0;
+        uint64_t n_off = 0;
+        if (nk < k1) {
+            n_len = slen[nk];
+            n_off = soff[nk];
+        }
+        auto next_segment = [&]() {                     // cursor -> first line of the next non-empty segment
+            while (nk < k1 && n_len == 0) {             // empty segments (rare)
+                if (++nk < k1) {
+                    n_len = slen[nk];
+                    n_off = soff[nk];
+                }
+            }
+            if (nk < k1) {
+                c_ss = uint32_t(dbase + n_off - lo);
+                c_se = c_ss + n_len;
+                c_line = c_ss & ~127u;
+                c_last = (c_se - 1) & ~127u;
+                if (++nk < k1) {                        // prefetch the one after (used a stage later)
+                    n_len = slen[nk];
+                    n_off = soff[nk];
+                }
+            } else {
+                c_line = kOOB;
+            }
+        };
+        auto advance = [&]() {
+            if (c_line == kOOB)
+                return;
+            if (c_line == c_last)
+                next_segment();
+            else
+                c_line += 128;
+        };
+        next_segment();
+        LineDesc d0, d1;                                // the lines in slots 0 and 1
+        d0 = LineDesc{c_line, c_ss, c_se};
+        advance();
+        d1 = LineDesc{c_line, c_ss, c_se};
+        advance();
+        issue_rows(rs, lds0, d0.line, lane);
+        issue_rows(rs, lds0 + kSlot, d1.line, lane);
+        uint32_t b = 0;
+        auto step = [&](uint32_t k, const uint32_t (&ad)[33], LineDesc &slot_d, uint32_t slot_lds) {
+            brb_dma::wait_vmcnt<0>();
+            uint32_t dw[33];
+            read_window(ad, dw);
+            const LineDesc d = slot_d;                  // line k-1
+            if (k + 1 < K) {                            // line k+1 into the slot of line k-1
+                slot_d = LineDesc{c_line, c_ss, c_se};
+                const uint32_t rel = c_line;
+                advance();
+                issue_rows(rs, slot_lds, rel, lane);
+            }
+            if (d.line != kOOB) {
+                const bool whole = d.ss < d.line && d.se - d.line >= 128u + b;
+                if (__builtin_amdgcn_ballot_w64(d.line != kOOB && !whole) == 0)
+                    emit_whole_line(f, b, dw);
+                else
+                    emit_range(f, d, b, dw);
+            }
+            f.pump();
+            f.pump();
+            f.pump();
+        };
+        for (uint32_t k = 1; k <= K; k += 2) {
+            step(k, win.ae, d0, lds0);
+            if (k == K)
+                break;
+            step(k + 1, win.ao, d1, lds0 + kSlot);
+        }
+        if (valid)
+            store_digest(out, rec, f.finish());
+    }
 }
 
 }  // namespace
@@ -100,7 +249,15 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
 {
     if (n_rec == 0)
         return hipSuccess;
-    md5_seg_kernel<<<unsigned((n_rec + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, soff, slen, first, n_rec, out);
+    if (brb_opt::get(brb_opt::kSegLine) == 0) {
+        md5_seg_kernel<<<unsigned((n_rec + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, soff, slen, first, n_rec, out);
+        return hipGetLastError();
+    }
+    constexpr int W = 4;                               // 4 x 32 KiB of LDS: one workgroup per CU
+    const uint64_t groups = (n_rec + 63) / 64;
+    const uint64_t wgs = (groups + W - 1) / W;
+    const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
+    md5_seg_line_kernel<W><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);
     return hipGetLastError();
 }
 

@@ -18,10 +18,11 @@ enum Opt {
     kB64Group = 5,      // -1: the launcher's choice; 0..6: log2 of the base64 lanes per record
     kHostChunkMiB = 6,  // 0: host-mode Blowfish/RC4 chunks of 16 MiB; k: k MiB (tools/host_sweep.py)
     kHostDigestChunkMiB = 7,   // 0: host-mode digest chunks of 32 MiB; k: k MiB
-    kCount = 8
+    kSegLine = 8,       // 1: segment digests / MetaData unpack on the line-staged kernels; 0: per-lane
+    kCount = 9
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

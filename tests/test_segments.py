@@ -41,17 +41,94 @@ def _want(orc, pool, offs, lens, first):
     return np.frombuffer(b"".join(out), np.uint8).reshape(-1, 16)
 
 
+@pytest.mark.parametrize("seg_line", [1, 0])
 @pytest.mark.parametrize("seed,n_rec,max_segs,max_len", [(1, 300, 5, 40), (2, 200, 20, 7), (3, 64, 3, 3000),
-                                                        (4, 1000, 1, 200), (5, 5, 200, 100)])
-def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len):
+                                                        (4, 1000, 1, 200), (5, 5, 200, 100), (6, 700, 40, 3),
+                                                        (7, 257, 8, 130)])
+def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len, seg_line):
+    """seg_line 1: the line-staged kernel (line_stream.h; round 4), 0: the per-lane block kernel."""
     pool, offs, lens, first = _case(seed, n_rec, max_segs, max_len)
     want = _want(orc, pool, offs, lens, first)
-    got = brb.md5_batch_segments(pool, offs, lens, first)
-    assert np.array_equal(got, want)
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(pool, offs, lens, first)
+        assert np.array_equal(got, want)
+        t = torch_dev
+        dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
+                                     t.from_numpy(first).cuda())
+        assert np.array_equal(dev.cpu().numpy(), want)
+
+
+def _pack_items_case(n, K, Q, gap, seed):
+    """The md5seg bench layout: record i = K items of Q bytes inside one pack, `gap` bytes between
+    items (the 24-byte item fields and the canary: 25), packs back to back."""
+    rng = np.random.default_rng(seed)
+    stride = 64 + K * (gap + Q)
+    pool = workload.gen_records(0x5EED00F6 + seed, 0, 1, n * stride + 64)
+    offs = (np.arange(n, dtype=np.uint64)[:, None] * stride + 64 + gap - 1
+            + np.arange(K, dtype=np.uint64)[None, :] * (gap + Q)).reshape(-1).astype(np.uint64)
+    lens = np.full(n * K, Q, np.uint32)
+    if seed % 2:                                  # ragged item sizes inside the same slots
+        lens = rng.integers(0, Q + 1, n * K).astype(np.uint32)
+    first = (np.arange(n + 1, dtype=np.uint64) * K).astype(np.uint64)
+    return pool, offs, lens, first
+
+
+@pytest.mark.parametrize("n,K,Q,gap,seed", [(65536, 4, 375, 25, 0), (4097, 4, 375, 25, 1), (3000, 9, 61, 3, 2),
+                                            (2000, 3, 700, 130, 3), (1024, 16, 4, 1, 4), (640, 2, 1, 0, 5)])
+def test_segments_pack_layout(brb, orc, torch_dev, n, K, Q, gap, seed):
+    """Segments as the MetaData items of back-to-back packs (the md5seg bench shape at full size
+    and variants: ragged sizes, items sharing memory lines, 1..4-byte items), line-staged kernel vs
+    the per-lane kernel vs hashlib on sampled records (every record for the smaller shapes)."""
     t = torch_dev
-    dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
-                                 t.from_numpy(first).cuda())
-    assert np.array_equal(dev.cpu().numpy(), want)
+    pool, offs, lens, first = _pack_items_case(n, K, Q, gap, seed)
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    d, o, ln, fi = dev(pool), dev(offs), dev(lens), dev(first)
+    got = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
+    with brb.TestOption("seg_line", 0):
+        ref = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
+    assert np.array_equal(got, ref)
+    idx = range(n) if n <= 4097 else list(range(0, n, 97)) + [n - 1]
+    for i in idx:
+        msg = b"".join(pool[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+                       for k in range(int(first[i]), int(first[i + 1])))
+        assert got[i].tobytes() == hashlib.md5(msg).digest(), i
+
+
+def test_segments_mixed_wide_groups(brb, torch_dev):
+    """One launch with groups whose segments lie within 2 GiB (line-staged) and groups whose
+    segments lie more than 2 GiB apart (32-bit DMA offsets cannot reach: the per-lane path), 640
+    records in 10 groups, every other group wide."""
+    t = torch_dev
+    far = (1 << 31) + 4099
+    size = far + (1 << 20)
+    d = t.empty(size, dtype=t.uint8, device="cuda")
+    lo_h = workload.gen_records(0x5EED00F7, 0, 1, 1 << 20)
+    hi_h = workload.gen_records(0x5EED00F8, 0, 1, 1 << 20)
+    d[: lo_h.size] = t.from_numpy(lo_h).cuda()
+    d[far:far + hi_h.size] = t.from_numpy(hi_h).cuda()
+    rng = np.random.default_rng(41)
+    n = 640
+    counts = rng.integers(1, 5, n)
+    first = np.zeros(n + 1, np.uint64)
+    first[1:] = np.cumsum(counts)
+    nseg = int(first[-1])
+    lens = rng.integers(0, 900, nseg).astype(np.uint32)
+    offs = rng.integers(0, (1 << 20) - 1000, nseg).astype(np.uint64)
+    wide = np.zeros(nseg, bool)
+    for g in range(1, 10, 2):                    # groups 1, 3, 5, 7, 9: one segment far away
+        r = 64 * g + 5
+        wide[int(first[r])] = True
+    offs[wide] += far
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
+    for i in range(n):
+        parts = []
+        for k in range(int(first[i]), int(first[i + 1])):
+            o, m = int(offs[k]), int(lens[k])
+            parts.append((hi_h[o - far:o - far + m] if o >= far else lo_h[o:o + m]).tobytes())
+        assert got[i].tobytes() == hashlib.md5(b"".join(parts)).digest(), i
+    del d
+    t.cuda.empty_cache()
 
 
 def test_segments_equal_streaming_oracle(brb, orc):
