@@ -118,29 +118,30 @@ struct LineDesc {
     uint32_t line, ss, se;
 };
 
-// Emits the message words of one range that start in the window's line k-1 (see the file comment).
-//   d      the line and its range (d.line != kOOB)
-//   b      the lane's word-grid phase inside lines (0..3), set at the range's first line
+// Emits the message words of one range that start in the window's line k-1 (see the file comment),
+// in line-relative byte coordinates:
+//   first  the range starts in this line, at byte ss (0..127); else it started in an earlier line
+//   endr   the range's end (exclusive), line-relative, > 0 (clamped: 4096 = "well past this line")
+//   b      the lane's word-grid phase inside lines (0..3), set here at the range's first line
 //   dw     the 33 window dwords
-// Whole words go to the funnel ring; if the range ends in this line, the bytes of its last partial
-// word become the carry.  Returns nothing; f.wpos / acc / nacc / total advance.
+// Whole words go to the funnel ring; when the range's last word starts in this line, the bytes of a
+// last partial word become the carry and the call returns true (the range is done).  The caller adds
+// the range's length to f.total.
 template <uint32_t RW>
-BRB_DEV void emit_range(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[33])
+BRB_DEV bool emit_range(brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32_t endr, uint32_t &b,
+                        const uint32_t (&dw)[33])
 {
-    const bool first = d.ss >= d.line;                        // the range starts in this line
     int o;                                                    // grid offset of the first word (-3..127)
     uint32_t e = 0;
     if (first) {
         e = f.nacc;
-        o = int(d.ss - d.line) - int(e);
+        o = int(ss) - int(e);
         b = uint32_t(o) & 3u;
-        f.total += d.se - d.ss;
     } else {
         o = int(b);
     }
-    const uint32_t endr = d.se - d.line < 4096u ? d.se - d.line : 4096u;   // range end, line-relative
     if (int(endr) <= o)                                       // its last word started in the line before
-        return;
+        return true;
     const int i0 = o >> 2;                                    // -1 .. 31
     const int span = int(endr) - int(b);                      // > 4 i0
     const int iw = span >> 2 < 32 ? span >> 2 : 32;           // whole words: i0 <= i < iw
@@ -167,6 +168,19 @@ BRB_DEV void emit_range(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b,
         f.nacc = rem;
         f.acc = rem ? (tail & ((1u << (8 * rem)) - 1u)) : 0u;
     }
+    return ends;
+}
+
+// The same for a staged segment line (md5_seg_kernels.hip): the range and the line in offsets from
+// the group's lowest line.
+template <uint32_t RW>
+BRB_DEV void emit_desc(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[33])
+{
+    const bool first = d.ss >= d.line;
+    if (first)
+        f.total += d.se - d.ss;
+    const uint32_t endr = d.se - d.line < 4096u ? d.se - d.line : 4096u;
+    emit_range(f, first, d.ss - d.line, endr, b, dw);
 }
 
 // All 32 words of a line that lies wholly inside the lane's current range, not its first line

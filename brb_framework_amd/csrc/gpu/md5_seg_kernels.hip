@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 if (__builtin_amdgcn_ballot_w64(d.line != kOOB && !whole) == 0)
                     emit_whole_line(f, b, dw);
                 else
-                    emit_range(f, d, b, dw);
+                    emit_desc(f, d, b, dw);
             }
             f.pump();
             f.pump();
