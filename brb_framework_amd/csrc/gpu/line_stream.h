@@ -39,9 +39,10 @@ constexpr uint32_t kRingWords = 64;       // funnel ring words per lane
 // the same window dword hit different banks.
 struct Win {
     uint32_t ae[33], ao[33];
+    uint32_t fr;                               // the lane's row in slot 0, OR its granule swizzle
     BRB_DEV void init(uint32_t slot0_lds, uint32_t lane)
     {
-        const uint32_t fr = (slot0_lds + lane * 128) | (((lane >> 1) & 7) << 4);
+        fr = (slot0_lds + lane * 128) | (((lane >> 1) & 7) << 4);
 #pragma unroll
         for (uint32_t j = 0; j < 33; j++) {
             const uint32_t q4 = 4 * j;
@@ -53,6 +54,13 @@ struct Win {
 };
 
 BRB_DEV uint32_t lds_ld(uint32_t a) { return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(a); }
+
+// Window dword j (0..63) at a lane-varying j: line k-1 in slot `par`, line k in the other.
+BRB_DEV uint32_t win_dword(const Win &w, uint32_t j, uint32_t par)
+{
+    const uint32_t q4 = 4 * j;
+    return lds_ld((((q4 & 124u) ^ w.fr) + ((q4 & 128u) << 6)) ^ (par ? kSlot : 0u));
+}
 
 // The 33 window dwords; returns once they are in registers (lgkmcnt(0)), so the slot of line k-1
 // may be refilled right after.

@@ -13,7 +13,10 @@
 // include/brb_crypto.h for the two rules where the reference reads past its buffer.
 #include "brb_kernels.h"
 #include "byte_stream.h"
+#include "digest_var_line.h"
+#include "line_stream.h"
 #include "md5_funnel.h"
+#include "test_options.h"
 
 namespace {
 
@@ -59,18 +62,12 @@ struct Ahead {
     BRB_DEV uint64_t qw(int i) const { return uint64_t(dw(i)) | (uint64_t(dw(i + 1)) << 32); }
 };
 
-__global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *__restrict__ data,
-                                                                 const uint64_t *__restrict__ offs,
-                                                                 const uint32_t *__restrict__ lens, uint64_t n,
-                                                                 BRB_MetaDataUnpackInfo *__restrict__ info)
+// MetaDataUnpack of one pack by one lane with per-lane loads (the round-3 kernel's walk): groups
+// whose packs span 2 GiB or more take it inside the line-staged kernel, and the round-3 kernel
+// (test option seg_line = 0) is this function per lane.
+template <uint32_t RW>
+BRB_DEV BRB_MetaDataUnpackInfo unpack_lane(brb_md5::FunnelT<RW> &f, const uint8_t *base, uint64_t size)
 {
-    __shared__ __attribute__((aligned(8192))) uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];   // 8 KiB per wave
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-    if (r >= n)
-        return;
-    const uint8_t *base = data + offs[r];
-    const uint64_t size = lens[r];
     int32_t code;
     uint32_t items = 0;
     uint64_t offset = 0, remaining = 0, needed = 0;   // cur_offset starts at the MemBuffer offset, 0
@@ -85,8 +82,6 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
         code = BRB_METADATA_UNPACK_FAILED_INVALID_HEADER_MAGIC;
     } else {
         offset = BRB_METADATA_HEADER_SIZE;                  // :198-199
-        brb_md5::Funnel f;
-        f.init(&blk[wave][0][lane]);
         code = BRB_METADATA_UNPACK_SUCCESS;
         uint64_t sz = hd.qw(20);                            // item 0's sz (bytes 80..87)
         for (int32_t i = 0; i < item_count; i++) {          // :202
@@ -159,7 +154,194 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
     o.cur_offset = offset;
     o.cur_remaining = remaining;
     o.cur_needed = needed;
-    info[r] = o;
+    return o;
+}
+
+__global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *__restrict__ data,
+                                                                 const uint64_t *__restrict__ offs,
+                                                                 const uint32_t *__restrict__ lens, uint64_t n,
+                                                                 BRB_MetaDataUnpackInfo *__restrict__ info)
+{
+    __shared__ __attribute__((aligned(8192))) uint32_t blk[kBlock / 64][brb_md5::kRingWords][64];   // 8 KiB per wave
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t r = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+    if (r >= n)
+        return;
+    brb_md5::Funnel f;
+    f.init(&blk[wave][0][lane]);
+    info[r] = unpack_lane(f, data + offs[r], lens[r]);
+}
+
+// Line-staged MetaDataUnpack (round 4; line_stream.h).  A wave unpacks groups of 64 packs, one per
+// lane; a pack's 128-byte lines stream through the two-slot LDS-DMA ring, and the lane walks its pack
+// out of the window (lines k-1, k) as a state machine over the reference's loop (meta_data.c:202-282):
+//   FIELDS at `offset`: the loop's checks, sz from the item's fields (window bytes), -> DATA
+//   DATA [ds, de):       the item's words that start in line k-1 emitted into the funnel ring;
+//                        -> CANARY once its last word is out
+//   CANARY at de:        the 0x1F check, items++, offset == size stops the walk, -> FIELDS
+// Every event is handled in the line that holds its first byte, so the window always holds what it
+// reads; the whole line's reads happen before that line's slot is refilled.  Per line up to 33
+// words go to the ring and up to three blocks are compressed.  The return codes and the unsigned
+// long arithmetic of cur_offset / cur_remaining / cur_needed are unpack_lane's (the reference's).
+template <int W>
+__global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__restrict__ data,
+                                                                const uint64_t *__restrict__ offs,
+                                                                const uint32_t *__restrict__ lens, uint64_t n,
+                                                                BRB_MetaDataUnpackInfo *__restrict__ info)
+{
+    using namespace brb_line;
+    constexpr uint32_t RW = brb_line::kRingWords;
+    enum : uint32_t { kFields = 0, kData = 1, kCanary = 2, kDone = 3 };
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * 2 * kSlot];
+    __shared__ __attribute__((aligned(16384))) uint32_t fring[W][RW][64];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n + 63) / 64;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * 2 * kSlot;
+    const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    Win win;
+    win.init(lds0, lane);
+
+    for (uint64_t g = uint64_t(blockIdx.x) * W + wv; g < n_groups; g += uint64_t(gridDim.x) * W) {
+        const uint64_t r = g * 64 + lane;
+        const bool valid = r < n;
+        const uint64_t base = valid ? dbase + offs[r] : dbase;
+        const uint64_t size = valid ? lens[r] : 0;
+        const uint32_t a0 = uint32_t(base & 127);
+        const uint32_t nl = size ? uint32_t((a0 + size + 127) >> 7) : 0u;
+        const uint64_t line0 = base & ~uint64_t(127);
+        const uint64_t lo = brb_digest::uniform64(brb_digest::wave_min64(nl ? line0 : ~uint64_t(0)));
+        const uint64_t hi = brb_digest::uniform64(brb_digest::wave_max64(nl ? line0 + 128 * uint64_t(nl) : 0));
+        const uint32_t Kl = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
+        const uint32_t K = Kl ? Kl : 1u;                  // iteration 1 reads every header
+        brb_md5::FunnelT<RW> f;
+        f.init(&fring[wv][0][lane]);
+        if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {   // no line, or too wide
+            if (valid)
+                info[r] = unpack_lane(f, reinterpret_cast<const uint8_t *>(base), size);
+            continue;
+        }
+        const brb_dma::v4i rs = group_rsrc(lo, hi);
+        const uint32_t rel0 = nl ? uint32_t(line0 - lo) : kOOB;
+        auto line_rel = [&](uint32_t j) { return j < nl ? rel0 + 128 * j : kOOB; };
+        issue_rows(rs, lds0, line_rel(0), lane);
+        issue_rows(rs, lds0 + kSlot, line_rel(1), lane);
+
+        int32_t code = BRB_METADATA_UNPACK_SUCCESS, item_count = 0, item = 0;
+        uint32_t items = 0, phase = kDone, b = 0, dig[4] = {0, 0, 0, 0};
+        uint64_t offset = 0, remaining = 0, needed = 0, ds = 0, de = 0;
+
+        auto step = [&](uint32_t k, const uint32_t (&ad)[33], uint32_t par, uint32_t slot_lds) {
+            brb_dma::wait_vmcnt<0>();
+            uint32_t dw[33];
+            read_window(ad, dw);
+            // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
+            const int64_t L0 = int64_t(128) * int64_t(k - 1) - int64_t(a0);
+            const int64_t L1 = L0 + 128;
+            auto rd32 = [&](int64_t p) -> uint32_t {           // pack bytes p .. p + 3, 0 past the pack
+                const uint32_t wb = uint32_t(p - L0);
+                const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, par),
+                                                             win_dword(win, wb >> 2, par), 8 * (wb & 3));
+                const uint64_t left = uint64_t(p) < size ? size - uint64_t(p) : 0;
+                return left >= 4 ? v : v & ((1u << (8 * uint32_t(left))) - 1u);
+            };
+            if (k == 1 && valid) {                               // MetaDataHeader (libbrb_data.h:322-330)
+                item_count = int32_t(rd32(4));
+                const uint64_t magic = uint64_t(rd32(16)) | (uint64_t(rd32(20)) << 32);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    dig[q] = rd32(24 + 4 * q);
+                if (magic != kMagic) {                           // meta_data.c:183-195
+                    code = BRB_METADATA_UNPACK_FAILED_INVALID_HEADER_MAGIC;
+                } else {
+                    offset = BRB_METADATA_HEADER_SIZE;           // :198-199
+                    phase = kFields;
+                }
+            }
+            bool more = phase != kDone;
+            while (more) {
+                more = false;
+                if (phase == kFields && int64_t(offset) < L1) {  // :202-246, the loop's top
+                    if (item >= item_count) {
+                        phase = kDone;
+                    } else {
+                        remaining = size - offset;               // :213
+                        if (remaining < kItemStruct) {           // :216-224
+                            needed = kItemStruct - remaining;
+                            code = BRB_METADATA_UNPACK_FAILED_NEED_MORE_DATA_METAITEM;
+                            phase = kDone;
+                        } else {
+                            const uint64_t sz = uint64_t(rd32(int64_t(offset) + 16)) |
+                                                (uint64_t(rd32(int64_t(offset) + 20)) << 32);
+                            offset += kItemRaw;                  // :227-232
+                            remaining -= kItemRaw;
+                            if (remaining < sz + 1 || sz > size) {   // :237-246
+                                needed = sz + 1 - remaining;
+                                code = BRB_METADATA_UNPACK_FAILED_NEED_MORE_DATA_OBJECT;
+                                phase = kDone;
+                            } else {
+                                ds = offset;
+                                de = offset + sz;
+                                f.total += sz;
+                                offset += sz;                    // :249-256 (the walk's values after the data)
+                                remaining -= sz;
+                                phase = kData;
+                                more = true;
+                            }
+                        }
+                    }
+                }
+                if (phase == kData && int64_t(ds) < L1) {        // :249-254 BRB_MD5UpdateBig of the data
+                    const bool first = int64_t(ds) >= L0;
+                    const int64_t er = int64_t(de) - L0;
+                    const bool done = de == ds ||
+                                      emit_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, dw);
+                    if (done) {
+                        phase = kCanary;
+                        more = true;
+                    }
+                }
+                if (phase == kCanary && int64_t(de) < L1) {      // :258-281
+                    if ((rd32(int64_t(de)) & 0xFFu) != 0x1Fu) {
+                        code = BRB_METADATA_UNPACK_FAILED_CORRUPTED_CANARY;
+                        phase = kDone;
+                    } else {
+                        offset += 1;
+                        remaining -= 1;
+                        items++;
+                        item++;
+                        phase = offset == size ? kDone : kFields;
+                        more = phase != kDone;
+                    }
+                }
+            }
+            if (k + 1 < K)                                       // line k+1 into the slot of line k-1
+                issue_rows(rs, slot_lds, phase == kDone ? kOOB : line_rel(k + 1), lane);
+            f.pump();
+            f.pump();
+            f.pump();
+        };
+        for (uint32_t k = 1; k <= K; k += 2) {
+            step(k, win.ae, 0, lds0);
+            if (k == K)
+                break;
+            step(k + 1, win.ao, 1, lds0 + kSlot);
+        }
+        if (!valid)
+            continue;
+        if (code == BRB_METADATA_UNPACK_SUCCESS) {               // :287-298
+            const Md5State st = f.finish();
+            if (st.a != dig[0] || st.b != dig[1] || st.c != dig[2] || st.d != dig[3])
+                code = BRB_METADATA_UNPACK_FAILED_DIGEST_INVALID;
+        }
+        BRB_MetaDataUnpackInfo o;
+        o.error_code = code;
+        o.item_count = items;
+        o.cur_offset = offset;
+        o.cur_remaining = remaining;
+        o.cur_needed = needed;
+        info[r] = o;
+    }
 }
 
 }  // namespace
@@ -171,7 +353,15 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
 {
     if (n == 0)
         return hipSuccess;
-    metadata_unpack_kernel<<<unsigned((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, offs, lens, n, info);
+    if (brb_opt::get(brb_opt::kSegLine) == 0) {
+        metadata_unpack_kernel<<<unsigned((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, offs, lens, n, info);
+        return hipGetLastError();
+    }
+    constexpr int W = 4;                               // 4 x 32 KiB of LDS: one workgroup per CU
+    const uint64_t groups = (n + 63) / 64;
+    const uint64_t wgs = (groups + W - 1) / W;
+    const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
+    metadata_line_kernel<W><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
     return hipGetLastError();
 }
 

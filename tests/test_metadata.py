@@ -157,24 +157,28 @@ def infos_as_tuples(info):
 
 
 @pytest.mark.gpu
-def test_unpack_batch_vs_oracle(brb, orc):
+@pytest.mark.parametrize("seg_line", [1, 0])
+def test_unpack_batch_vs_oracle(brb, orc, seg_line):
+    """seg_line 1: the line-staged kernel (round 4), 0: the per-lane kernel."""
     packs = corpus(3, 4000)
     rng = np.random.default_rng(4)
     buf, offs, lens = scatter(rng, packs)
     want = [orc.metadata_unpack(p) for p in packs]
-    got = infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens))      # host mode
-    assert got == want
-    import torch
-    d = torch.from_numpy(buf).cuda()
-    o = torch.from_numpy(offs.view(np.int64)).cuda()
-    ln = torch.from_numpy(lens.view(np.int32)).cuda()
-    dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
-    assert infos_as_tuples(dev) == want
-    assert infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens, all_devices=True)) == want
+    with brb.TestOption("seg_line", seg_line):
+        got = infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens))      # host mode
+        assert got == want
+        import torch
+        d = torch.from_numpy(buf).cuda()
+        o = torch.from_numpy(offs.view(np.int64)).cuda()
+        ln = torch.from_numpy(lens.view(np.int32)).cuda()
+        dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+        assert infos_as_tuples(dev) == want
+        assert infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens, all_devices=True)) == want
 
 
 @pytest.mark.gpu
-def test_unpack_batch_bench_count(brb, orc):
+@pytest.mark.parametrize("seg_line", [1, 0])
+def test_unpack_batch_bench_count(brb, orc, seg_line):
     """A bench-sized batch: 65 536 valid and mutated packs (every return code) at arbitrary byte
     offsets, device mode, every BRB_MetaDataUnpackInfo field against the oracle."""
     import torch
@@ -184,9 +188,35 @@ def test_unpack_batch_bench_count(brb, orc):
     d = torch.from_numpy(buf).cuda()
     o = torch.from_numpy(offs.view(np.int64)).cuda()
     ln = torch.from_numpy(lens.view(np.int32)).cuda()
-    dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    with brb.TestOption("seg_line", seg_line):
+        dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
     assert infos_as_tuples(dev) == want
     assert len({w[0] for w in want}) >= 5                     # the corpus reaches the return codes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_items,item_len,gap", [(4, 375, 0), (9, 61, 3), (40, 2, 1), (2, 1000, 77), (13, 0, 5)])
+def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap):
+    """Batches whose packs share one layout (the bench's 4 x 375-byte items, and tiny / empty /
+    large items), so every lane of a wave reaches its events in the same line; packs back to back
+    or with `gap` bytes between them; 20 % carry a flipped byte; every field vs the oracle."""
+    rng = np.random.default_rng(n_items * 1000 + item_len)
+    packs = []
+    for i in range(5000):
+        items = [(j, i, rng.integers(0, 256, item_len, dtype=np.uint8).tobytes()) for j in range(n_items)]
+        p = bytearray(build(items))
+        if rng.random() < 0.2:
+            p[int(rng.integers(0, len(p)))] ^= 1 << int(rng.integers(0, 8))
+        packs.append(bytes(p))
+    parts, offs, pos = [], [], 0
+    for p in packs:
+        offs.append(pos)
+        parts.append(p + bytes(gap))
+        pos += len(p) + gap
+    buf = np.frombuffer(b"".join(parts) + b"\0", np.uint8).copy()
+    lens = np.array([len(p) for p in packs], np.uint32)
+    got = infos_as_tuples(brb.metadata_unpack_batch(buf, np.array(offs, np.uint64), lens))
+    assert got == [orc.metadata_unpack(p) for p in packs]
 
 
 @pytest.mark.gpu
@@ -205,7 +235,8 @@ def test_pack_batch_round_trip(brb, orc):
 
 
 @pytest.mark.gpu
-def test_unpack_large_items(brb, orc):
+@pytest.mark.parametrize("seg_line", [1, 0])
+def test_unpack_large_items(brb, orc, seg_line):
     """Items of 64 KiB .. 1 MiB (many MD5 blocks per lane, items spanning block boundaries at every
     byte offset) next to tiny packs in the same batch."""
     rng = np.random.default_rng(6)
@@ -215,7 +246,9 @@ def test_unpack_large_items(brb, orc):
         p = build(items)
         packs += [p, mutate(rng, items, p)]
     buf, offs, lens = scatter(rng, packs)
-    assert infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens)) == [orc.metadata_unpack(p) for p in packs]
+    with brb.TestOption("seg_line", seg_line):
+        got = infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens))
+    assert got == [orc.metadata_unpack(p) for p in packs]
 
 
 @pytest.mark.gpu
