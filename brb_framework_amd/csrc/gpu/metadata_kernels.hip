@@ -231,33 +231,19 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         uint32_t items = 0, phase = kDone, b = 0, dig[4] = {0, 0, 0, 0};
         uint64_t offset = 0, remaining = 0, needed = 0, ds = 0, de = 0;
 
-        auto step = [&](uint32_t k, const uint32_t (&ad)[33], uint32_t par, uint32_t slot_lds) {
-            brb_dma::wait_vmcnt<0>();
-            uint32_t dw[33];
-            read_window(ad, dw);
-            // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
-            const int64_t L0 = int64_t(128) * int64_t(k - 1) - int64_t(a0);
-            const int64_t L1 = L0 + 128;
+        // The walk's events whose first byte lies before pack byte L1, line k-1 = pack bytes [L0, L1)
+        // in the window.  drain: after the last line, the events a pack shorter than its header
+        // still reaches past its end (every byte there reads as 0: sz 0, no canary).
+        auto events = [&](int64_t L0, int64_t L1, uint32_t par, const uint32_t (&dw)[33], bool drain) {
             auto rd32 = [&](int64_t p) -> uint32_t {           // pack bytes p .. p + 3, 0 past the pack
+                if (drain || uint64_t(p) >= size)
+                    return 0u;
                 const uint32_t wb = uint32_t(p - L0);
                 const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, par),
                                                              win_dword(win, wb >> 2, par), 8 * (wb & 3));
-                const uint64_t left = uint64_t(p) < size ? size - uint64_t(p) : 0;
+                const uint64_t left = size - uint64_t(p);
                 return left >= 4 ? v : v & ((1u << (8 * uint32_t(left))) - 1u);
             };
-            if (k == 1 && valid) {                               // MetaDataHeader (libbrb_data.h:322-330)
-                item_count = int32_t(rd32(4));
-                const uint64_t magic = uint64_t(rd32(16)) | (uint64_t(rd32(20)) << 32);
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    dig[q] = rd32(24 + 4 * q);
-                if (magic != kMagic) {                           // meta_data.c:183-195
-                    code = BRB_METADATA_UNPACK_FAILED_INVALID_HEADER_MAGIC;
-                } else {
-                    offset = BRB_METADATA_HEADER_SIZE;           // :198-199
-                    phase = kFields;
-                }
-            }
             bool more = phase != kDone;
             while (more) {
                 more = false;
@@ -294,12 +280,11 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                 if (phase == kData && int64_t(ds) < L1) {        // :249-254 BRB_MD5UpdateBig of the data
                     const bool first = int64_t(ds) >= L0;
                     const int64_t er = int64_t(de) - L0;
-                    const bool done = de == ds ||
+                    const bool done = de == ds || drain ||
                                       emit_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, dw);
-                    if (done) {
+                    more = done;                                 // else the line is used up (no second emission)
+                    if (done)
                         phase = kCanary;
-                        more = true;
-                    }
                 }
                 if (phase == kCanary && int64_t(de) < L1) {      // :258-281
                     if ((rd32(int64_t(de)) & 0xFFu) != 0x1Fu) {
@@ -315,6 +300,36 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                     }
                 }
             }
+        };
+        auto step = [&](uint32_t k, const uint32_t (&ad)[33], uint32_t par, uint32_t slot_lds) {
+            brb_dma::wait_vmcnt<0>();
+            uint32_t dw[33];
+            read_window(ad, dw);
+            // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
+            const int64_t L0 = int64_t(128) * int64_t(k - 1) - int64_t(a0);
+            if (k == 1 && valid) {                               // MetaDataHeader (libbrb_data.h:322-330)
+                auto hd32 = [&](uint32_t p) -> uint32_t {        // header bytes: 0 past the pack
+                    if (p >= size)
+                        return 0u;
+                    const uint32_t wb = p + a0;
+                    const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, par),
+                                                                 win_dword(win, wb >> 2, par), 8 * (wb & 3));
+                    const uint64_t left = size - p;
+                    return left >= 4 ? v : v & ((1u << (8 * uint32_t(left))) - 1u);
+                };
+                item_count = int32_t(hd32(4));
+                const uint64_t magic = uint64_t(hd32(16)) | (uint64_t(hd32(20)) << 32);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    dig[q] = hd32(24 + 4 * q);
+                if (magic != kMagic) {                           // meta_data.c:183-195
+                    code = BRB_METADATA_UNPACK_FAILED_INVALID_HEADER_MAGIC;
+                } else {
+                    offset = BRB_METADATA_HEADER_SIZE;           // :198-199
+                    phase = kFields;
+                }
+            }
+            events(L0, L0 + 128, par, dw, false);
             if (k + 1 < K)                                       // line k+1 into the slot of line k-1
                 issue_rows(rs, slot_lds, phase == kDone ? kOOB : line_rel(k + 1), lane);
             f.pump();
@@ -326,6 +341,10 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
             if (k == K)
                 break;
             step(k + 1, win.ao, 1, lds0 + kSlot);
+        }
+        if (phase != kDone) {                                    // a pack shorter than its header
+            uint32_t dw[33] = {};
+            events(int64_t(1) << 62, int64_t(1) << 62, 0, dw, true);
         }
         if (!valid)
             continue;
