@@ -161,6 +161,45 @@ def compute_fraction(path, key, launch_s, cyc_lone):
     return out
 
 
+ISSUE_CYC_LONE = 4.3   # shader cycles per issued instruction of a lone wave (tools/mb/md5_occ.hip, valu_mix.hip)
+ISSUE_CYC_W2 = 4.05    # per SIMD with two or more waves sharing it (the MD5 mix, tools/mb/valu_mix.hip)
+
+
+def issue_compute(path, key, launch_s, dispatches=1):
+    """roofline.compute for the lines that run one wave per SIMD and are bound by that wave's
+    instruction issue rather than by HBM (RC4 and frame/open, MetaData unpack, segment digests,
+    variable-length digests).  From the kept --pmc pass of the same kernel
+    (per dispatch; `dispatches` per step):
+      issued_per_simd  (SQ_INSTS_VALU + SQ_INSTS_LDS + SQ_INSTS_SALU) / 1024 SIMDs
+      frac_issue_ceiling  issued_per_simd x cycles per instruction / (launch time x CLOCK_GHZ): the
+                       share of the launch the SIMD needs just to issue those instructions at the
+                       measured rate -- ISSUE_CYC_LONE for one wave per SIMD, ISSUE_CYC_W2 for two or
+                       more (1.0 = issue-bound with no slack);
+      issue_busy_frac  SQ_ACTIVE_INST_ANY x 4 / 1024 / (GRBM_GUI_ACTIVE / 8): the share of dispatch
+                       cycles each SIMD had a wave issuing (clock-free);
+      wait_frac / wait_inst_frac  SQ_WAIT_ANY / SQ_WAVE_CYCLES (waiting on memory or LDS data) and
+                       SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waiting for an issue slot)."""
+    _, det = load_pmc(path, key)
+    if not det or "sq_insts_valu" not in det:
+        return None
+    per_launch = launch_s / dispatches
+    insts = det["sq_insts_valu"] + det.get("sq_insts_lds", 0) + det.get("sq_insts_salu", 0)
+    per_simd = insts / SIMDS
+    wps = det.get("sq_waves", SIMDS) / SIMDS            # waves per SIMD (every wave resident at once here)
+    cyc = ISSUE_CYC_LONE if wps < 1.5 else ISSUE_CYC_W2
+    out = {"bound": "simd issue", "issued_per_simd": round(per_simd, 1),
+           "valu_per_simd": round(det["sq_insts_valu"] / SIMDS, 1), "waves_per_simd": round(wps, 2),
+           "cycles_per_inst": cyc, "clock_ghz": CLOCK_GHZ,
+           "frac_issue_ceiling": round(per_simd * cyc / (per_launch * CLOCK_GHZ * 1e9), 4),
+           "source": det.get("source")}
+    if "sq_active_inst_any" in det and det.get("grbm_gui_active"):
+        out["issue_busy_frac"] = round(det["sq_active_inst_any"] * 4 / SIMDS / (det["grbm_gui_active"] / 8), 4)
+    if det.get("sq_wave_cycles"):
+        out["wait_frac"] = round(det.get("sq_wait_any", 0) / det["sq_wave_cycles"], 4)
+        out["wait_inst_frac"] = round(det.get("sq_wait_inst_any", 0) / det["sq_wave_cycles"], 4)
+    return out
+
+
 def main():
     args = parse()
     if args.config == 1:          # plumbing, no GPU (BASELINE cfg1)
@@ -877,6 +916,8 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                      "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      **traffic_fields(args.pmc_summary, f"f1_{args.op}"),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
+                     "compute": issue_compute(args.pmc_summary, f"f1_{args.op}", step_s,
+                                              2 if args.op == "rc4md5" else 1),
                      "note": "algorithmic bytes read+written per step; the bound in practice is the per-byte "
                              "RC4 dependency chain through LDS (DESIGN.md)"},
     }
@@ -989,7 +1030,8 @@ def bench_var(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         "roofline": {"bound": "hbm", "achieved": round(payload / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(payload / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      **traffic_fields(args.pmc_summary, f"var_{args.op}"),
-                     "launch_us_avg": round(step_s * 1e6, 2), "bytes_per_launch": payload},
+                     "launch_us_avg": round(step_s * 1e6, 2), "bytes_per_launch": payload,
+                     "compute": issue_compute(args.pmc_summary, f"var_{args.op}", step_s)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle     # test infrastructure: the CPU restatement is the baseline, never the product
@@ -1139,6 +1181,8 @@ def bench_f4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
                      "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      **traffic_fields(args.pmc_summary, f"f4_{args.op}"),
                      "step_us_avg": round(step_s * 1e6, 2), "bytes_per_step": moved,
+                     "compute": (issue_compute(args.pmc_summary, f"f4_{args.op}", step_s,
+                                               2 if args.op == "base64" else 1)),
                      "note": ("algorithmic bytes read + written per step; base64: 32 lanes per record, 12/16-byte "
                               "pieces, 8 waves per SIMD (HBM-bound, DESIGN.md 4.5)" if args.op == "base64" else
                               "algorithmic bytes read + written per step; one lane per record, so the bound in "

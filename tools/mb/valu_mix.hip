@@ -63,6 +63,34 @@ __global__ __launch_bounds__(256) void k(unsigned *out, unsigned long long *clk,
                OPS8(ALB(0), ALB(1), ALB(2), ALB(3), ADD(4), ADD(5), ADD(6), ADD(7));)
         }
         if constexpr (P == 15) { R16(OPS8(ALB(0), ALB(1), ADD(2), ADD(3), ALB(4), ALB(5), ADD(6), ADD(7));) }
+        // fast-heavy mixes.  5 fast : 1 slow and 4 : 1 as 8 independent chains
+        // (a 6- / 5-instruction pattern over 8 registers, 24 / 40 instructions per unit)
+        if constexpr (P == 16) {   // 5 : 1 -- 48 instructions per unit
+            R4(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADD(4), ALB(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ALB(2), ADD(3), ADD(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ALB(0), ADD(1), ADD(2), ADD(3), ADD(4), ADD(5), ADD(6), ALB(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ALB(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ALB(1), ADD(2), ADD(3), ADD(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ALB(3), ADD(4), ADD(5), ALB(6), ADD(7));)
+        }
+        if constexpr (P == 17) { R16(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ALB(4), ADD(5), ADD(6), ADD(7));)
+                                 R16(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADD(4), ADD(5), ADD(6), ALB(7));) }   // 7 : 1
+        if constexpr (P == 18) {   // 4 : 1 -- 40 instructions per unit
+            R4(OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ALB(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ALB(0), ADD(1), ADD(2), ADD(3), ADD(4), ADD(5), ALB(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ALB(2), ADD(3), ADD(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADD(4), ALB(5), ADD(6), ALB(7));
+               OPS8(ADD(0), ALB(1), ADD(2), ALB(3), ADD(4), ADD(5), ADD(6), ADD(7));)
+        }
+        // the split MD5 step over 8 chains: add(literal) bitop3 add add alignbit add (5 fast : 1 slow)
+        if constexpr (P == 19) {
+            R4(OPS8(ADDL(0), ADDL(1), ADDL(2), ADDL(3), BOP(4, 5), BOP(5, 6), BOP(6, 7), BOP(7, 0));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADD(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ALB(4), ALB(5), ALB(6), ALB(7));
+               OPS8(BOP(0, 1), BOP(1, 2), BOP(2, 3), BOP(3, 4), ADD(4), ADD(5), ADD(6), ADD(7));
+               OPS8(ADD(0), ADD(1), ADD(2), ADD(3), ADDL(4), ADDL(5), ADDL(6), ADDL(7));
+               OPS8(ALB(0), ALB(1), ALB(2), ALB(3), ADD(4), ADD(5), ADD(6), ADD(7));)
+        }
     }
     const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] = a + b + c + d + e + f + g + h;
@@ -72,7 +100,8 @@ __global__ __launch_bounds__(256) void k(unsigned *out, unsigned long long *clk,
     }
 }
 
-constexpr int INSTR_PER_ITER[16] = {128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 160, 128};
+constexpr int INSTR_PER_ITER[20] = {128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 128, 160, 128,
+                                    192, 256, 160, 192};
 
 template <int P>
 int run(const char *name, int W, int cus)
@@ -129,6 +158,10 @@ int main()
         run<12>("add/bitop3 alternating", W, cus);
         run<13>("perm/add alternating", W, cus);
         run<14>("MD5 mix (8 chains)", W, cus);
+        run<18>("4 add : 1 alignbit", W, cus);
+        run<16>("5 add : 1 alignbit", W, cus);
+        run<17>("7 add : 1 alignbit", W, cus);
+        run<19>("split MD5 step (5 fast : 1 slow)", W, cus);
     }
     return 0;
 }
