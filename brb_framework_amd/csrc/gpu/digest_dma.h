@@ -186,6 +186,65 @@ __global__ __launch_bounds__(64 * WAVES) void digest_fixed_dma_kernel(const uint
     BRB_LINE_PROBE(3);
 }
 
+// Records of exactly 64 bytes (cfg3: 1 Mi x 64 B): one data block and the constant padding block
+// per record, one 64-byte stage per group.  The generic kernel above spends ~100 scalar
+// instructions per group on its stage cursor (64-bit multiplies by the runtime record length, the
+// group-boundary bookkeeping of multi-stage records, the tail machinery) -- 1.70 M SALU per launch,
+// 17 % of the VALU count, issued by the same four waves per SIMD that the VALU-bound compression
+// keeps busy (profiles/r03_pmc_cfg3_md5.txt).  Here a wave walks its groups
+// w, w + W_total, ... with the byte stride between them fixed once, so a group costs one 64-bit add
+// and subtract, the descriptor and four DMAs.
+template <class Alg, int WAVES, bool OUT_ALIGNED>
+__global__ __launch_bounds__(64 * WAVES) void digest_b64_kernel(const uint8_t *__restrict__ data, uint64_t n_rec,
+                                                                uint8_t *__restrict__ out)
+{
+    using SG = brb_dma::Stager<1, false>;                     // 64-byte rows, 4 DMAs per stage
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SG::SLOT];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    uint64_t g = uint64_t(blockIdx.x) * WAVES + wv;
+    const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
+    if (g >= n_groups)
+        return;
+    uint8_t *my = ring + wv * (2 * SG::SLOT);
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(my));
+    const uint64_t last_full = n_rec / 64;                    // groups below this one hold 64 records
+    SG sg;
+    sg.init(64, uint32_t(g < last_full ? 64 : n_rec - g * 64), lane, true);
+    const uint64_t gbytes = wstride * 4096;                   // bytes from one of this wave's groups to the next
+    const uint8_t *base = data + g * 4096;
+    uint64_t left = (n_rec - g * 64) * 64;
+    sg.issue_fast(brb_dma::make_rsrc(base, left), lds0);
+    uint32_t slot = 0;
+    for (;;) {
+        const uint64_t gn = g + wstride;
+        const bool more = gn < n_groups;
+        if (more) {
+            base += gbytes;
+            left -= gbytes;
+            if (gn >= last_full)                              // the batch's partial last group
+                sg.group_offsets(64, uint32_t(n_rec - gn * 64), true);
+            sg.issue_fast(brb_dma::make_rsrc(base, left), slot ? lds0 : lds0 + SG::SLOT);
+            brb_dma::wait_vmcnt<SG::NI>();
+        } else {
+            brb_dma::wait_vmcnt<0>();
+        }
+        uint32_t w[16];
+        sg.read(my + slot * SG::SLOT, 0, w);
+        typename Alg::State st = Alg::iv();
+        Alg::compress(st, w);
+        Alg::pad_only(st, 64);
+        const uint64_t r = g * 64 + lane;
+        if (g < last_full || r < n_rec)
+            Alg::template store<OUT_ALIGNED>(out, r, st);
+        if (!more)
+            break;
+        g = gn;
+        slot ^= 1;
+    }
+}
+
 // Host-side launch.
 inline bool dma_supported(uint32_t rec_len)
 {
@@ -226,6 +285,13 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
             digest_fixed_dma_kernel<Alg, 8, 2, 2, true, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
         else
             digest_fixed_dma_kernel<Alg, 8, 2, 2, false, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
+    } else if (rec_len == 64 && brb_opt::get(brb_opt::kB64Kernel) != 0) {
+        // the lean 64-byte kernel, same shape as below (4 workgroups of 4 waves per CU, 16 KiB each)
+        const unsigned g = unsigned(wgs_needed < 1024 ? wgs_needed : 1024);
+        if (out_al)
+            digest_b64_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, n_rec, out);
+        else
+            digest_b64_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, n_rec, out);
     } else {
         // 4 workgroups per CU (32 KiB each), static groups: 1 Mi x 64 B = 16 384 groups = exactly 4
         // per wave.  Measured (md5_ab, 1 Mi x 64 B): 24.6 us; one 16-wave workgroup per CU with

@@ -19,10 +19,11 @@ enum Opt {
     kHostChunkMiB = 6,  // 0: host-mode Blowfish/RC4 chunks of 16 MiB; k: k MiB (tools/host_sweep.py)
     kHostDigestChunkMiB = 7,   // 0: host-mode digest chunks of 32 MiB; k: k MiB
     kSegLine = 8,       // 1: segment digests / MetaData unpack on the line-staged kernels; 0: per-lane
-    kCount = 9
+    kB64Kernel = 9,     // 1: 64-byte fixed-stride records on digest_b64_kernel; 0: the generic DMA kernel
+    kCount = 10
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1, 1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -388,7 +388,9 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k <= 16
  * parts, part g on device g % count; an all-devices batcher takes at most 16 parts either way), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
  * forced to 2^value), "host_chunk_mib" / "host_digest_chunk_mib" 0/k (host-mode chunks of the default
- * 16 / 32 MiB, or k MiB; chunk-size sweeps).  Returns 1 and the previous
+ * 16 / 32 MiB, or k MiB; chunk-size sweeps), "seg_line" 1/0 (segment digests and MetaData unpack on the
+ * line-staged kernels / the per-lane kernels), "b64_kernel" 1/0 (64-byte fixed-stride records on the
+ * lean 64-byte kernel / the generic one).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */
