@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
 // a lane's VIRTUAL lines are its non-empty segments' 128-byte memory lines in order, staged two
 // ahead by LDS-DMA into a two-slot ring.  Per line: the 33-dword window, the next stage issued, the
 // segment's words that start in this line emitted into the lane's 64-word funnel ring, and up to
-// three 16-word blocks compressed.  W waves per workgroup, W * 32 KiB of LDS; groups strided over
+// three 16-word blocks compressed.  W waves per workgroup, W * 38 KiB of LDS; groups strided over
 // the grid.
 template <int W>
 __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__restrict__ data,
@@ -120,8 +120,11 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
 {
     using namespace brb_line;
     constexpr uint32_t RW = brb_line::kRingWords;
+    constexpr uint32_t kTab = 512;                      // segments per group held in LDS (8 per record)
     __shared__ __attribute__((aligned(16384))) uint8_t ring[W * 2 * kSlot];
     __shared__ __attribute__((aligned(16384))) uint32_t fring[W][RW][64];
+    __shared__ uint64_t tab_off[W][kTab];
+    __shared__ uint32_t tab_len[W][kTab];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
@@ -134,14 +137,41 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         const uint64_t rec = g * 64 + lane;
         const bool valid = rec < n_rec;
         const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
-        // the group's line span and every lane's line count
+        brb_md5::FunnelT<RW> f;
+        f.init(&fring[wv][0][lane]);
+        // The group's segments are one contiguous range of the arrays (first[] is monotone):
+        // [s0, s1).  They go to this wave's LDS table with coalesced loads, so the stage cursor
+        // below reads them with LDS latency and no vector-memory load ever sits between a wave's
+        // DMA issues (a per-lane load there made hipcc wait for it right before the DMA).  A group
+        // with more segments takes the per-lane path.
+        const uint64_t s0 = brb_digest::uniform64(brb_digest::wave_min64(valid ? k0 : ~uint64_t(0)));
+        const uint64_t s1 = brb_digest::uniform64(brb_digest::wave_max64(valid ? k1 : 0));
+        const uint64_t S = s1 > s0 ? s1 - s0 : 0;
+        if (S > kTab) {
+            if (valid) {
+                seg_lane(f, data, soff, slen, k0, k1);
+                store_digest(out, rec, f.finish());
+            }
+            continue;
+        }
+        for (uint32_t i = lane; i < uint32_t(S); i += 64) {
+            tab_off[wv][i] = soff[s0 + i];
+            tab_len[wv][i] = slen[s0 + i];
+        }
+        __builtin_amdgcn_s_waitcnt(0);                  // the table is in LDS, every load of it done
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t t0 = uint32_t(k0 - (valid ? s0 : k0)), t1 = uint32_t(k1 - (valid ? s0 : k1));
+        // the group's line span and every lane's stage count (an empty segment costs its lane one
+        // empty stage)
         uint64_t lo = ~uint64_t(0), hi = 0;
         uint32_t nl = 0;
-        for (uint64_t kk = k0; kk < k1; kk++) {
-            const uint32_t len = slen[kk];
-            if (!len)
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t len = tab_len[wv][t];
+            if (!len) {
+                nl++;
                 continue;
-            const uint64_t a = dbase + soff[kk];
+            }
+            const uint64_t a = dbase + tab_off[wv][t];
             const uint64_t l0 = a & ~uint64_t(127), l1 = (a + len + 127) & ~uint64_t(127);
             lo = l0 < lo ? l0 : lo;
             hi = l1 > hi ? l1 : hi;
@@ -150,8 +180,6 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         lo = brb_digest::uniform64(brb_digest::wave_min64(lo));
         hi = brb_digest::uniform64(brb_digest::wave_max64(hi));
         const uint32_t K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
-        brb_md5::FunnelT<RW> f;
-        f.init(&fring[wv][0][lane]);
         if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {   // no line, or too wide
             if (valid) {
                 seg_lane(f, data, soff, slen, k0, k1);
@@ -161,49 +189,28 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         }
         const brb_dma::v4i rs = group_rsrc(lo, hi);      // K >= 1 here (some lane has a line)
 
-        // stage cursor: the next line to stage (offset from lo) and the segment it belongs to
-        uint32_t c_line = kOOB, c_last = 0, c_ss = 0, c_se = 0;
-        uint64_t nk = k0;                               // the next candidate segment, prefetched
-        uint32_t n_len = 0;
-        uint64_t n_off = 0;
-        if (nk < k1) {
-            n_len = slen[nk];
-            n_off = soff[nk];
-        }
-        auto next_segment = [&]() {                     // cursor -> first line of the next non-empty segment
-            while (nk < k1 && n_len == 0) {             // empty segments (rare)
-                if (++nk < k1) {
-                    n_len = slen[nk];
-                    n_off = soff[nk];
+        // Stage cursor: the line to stage next (offset from lo; kEnd: the cursor must enter the next
+        // segment first) and its segment; nt = the next table entry to enter.
+        constexpr uint32_t kEnd = 0xFFFFFFFFu;
+        uint32_t c_line = kEnd, c_last = 0, c_ss = 0, c_se = 0, nt = t0;
+        auto stage_line = [&]() -> LineDesc {                   // this stage's line; the cursor moves on
+            if (c_line == kEnd && nt < t1) {                    // enter segment nt
+                const uint32_t len = tab_len[wv][nt];
+                if (len) {
+                    c_ss = uint32_t(dbase + tab_off[wv][nt] - lo);
+                    c_se = c_ss + len;
+                    c_line = c_ss & ~127u;
+                    c_last = (c_se - 1) & ~127u;
                 }
+                nt++;
             }
-            if (nk < k1) {
-                c_ss = uint32_t(dbase + n_off - lo);
-                c_se = c_ss + n_len;
-                c_line = c_ss & ~127u;
-                c_last = (c_se - 1) & ~127u;
-                if (++nk < k1) {                        // prefetch the one after (used a stage later)
-                    n_len = slen[nk];
-                    n_off = soff[nk];
-                }
-            } else {
-                c_line = kOOB;
-            }
+            const LineDesc d{c_line == kEnd ? kOOB : c_line, c_ss, c_se};
+            if (c_line != kEnd)
+                c_line = c_line == c_last ? kEnd : c_line + 128;
+            return d;
         };
-        auto advance = [&]() {
-            if (c_line == kOOB)
-                return;
-            if (c_line == c_last)
-                next_segment();
-            else
-                c_line += 128;
-        };
-        next_segment();
-        LineDesc d0, d1;                                // the lines in slots 0 and 1
-        d0 = LineDesc{c_line, c_ss, c_se};
-        advance();
-        d1 = LineDesc{c_line, c_ss, c_se};
-        advance();
+        LineDesc d0 = stage_line();                             // the lines in slots 0 and 1
+        LineDesc d1 = stage_line();
         issue_rows(rs, lds0, d0.line, lane);
         issue_rows(rs, lds0 + kSlot, d1.line, lane);
         uint32_t b = 0;
@@ -213,10 +220,8 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
             read_window(ad, dw);
             const LineDesc d = slot_d;                  // line k-1
             if (k + 1 < K) {                            // line k+1 into the slot of line k-1
-                slot_d = LineDesc{c_line, c_ss, c_se};
-                const uint32_t rel = c_line;
-                advance();
-                issue_rows(rs, slot_lds, rel, lane);
+                slot_d = stage_line();
+                issue_rows(rs, slot_lds, slot_d.line, lane);
             }
             if (d.line != kOOB) {
                 const bool whole = d.ss < d.line && d.se - d.line >= 128u + b;
@@ -253,7 +258,7 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
         md5_seg_kernel<<<unsigned((n_rec + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, soff, slen, first, n_rec, out);
         return hipGetLastError();
     }
-    constexpr int W = 4;                               // 4 x 32 KiB of LDS: one workgroup per CU
+    constexpr int W = 4;                               // 4 x 38 KiB of LDS: one workgroup per CU
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());

@@ -329,7 +329,16 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                     phase = kFields;
                 }
             }
-            events(L0, L0 + 128, par, dw, false);
+            // the common line: every walking lane is inside an item's data that covers the whole
+            // line (not its first line, not its last word) -> 32 whole words, no event to look for
+            const bool whole = phase == kDone ||
+                               (phase == kData && int64_t(ds) < L0 && int64_t(de) - L0 >= 128 + int64_t(b));
+            if (k > 1 && __builtin_amdgcn_ballot_w64(!whole) == 0) {
+                if (phase == kData)
+                    emit_whole_line(f, b, dw);
+            } else {
+                events(L0, L0 + 128, par, dw, false);
+            }
             if (k + 1 < K)                                       // line k+1 into the slot of line k-1
                 issue_rows(rs, slot_lds, phase == kDone ? kOOB : line_rel(k + 1), lane);
             f.pump();
