@@ -224,7 +224,9 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 issue_rows(rs, slot_lds, slot_d.line, lane);
             }
             if (d.line != kOOB) {
-                const bool whole = d.ss < d.line && d.se - d.line >= 128u + b;
+                // whole line inside the segment, and not the line of its last word (emit_range sets
+                // the carry there)
+                const bool whole = d.ss < d.line && d.se - d.line > 128u + b;
                 if (__builtin_amdgcn_ballot_w64(d.line != kOOB && !whole) == 0)
                     emit_whole_line(f, b, dw);
                 else

@@ -330,9 +330,10 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                 }
             }
             // the common line: every walking lane is inside an item's data that covers the whole
-            // line (not its first line, not its last word) -> 32 whole words, no event to look for
+            // line and goes on past its 32 words (not its first line, not the line of its last word,
+            // which emit_range must see to set the carry) -> 32 whole words, no event to look for
             const bool whole = phase == kDone ||
-                               (phase == kData && int64_t(ds) < L0 && int64_t(de) - L0 >= 128 + int64_t(b));
+                               (phase == kData && int64_t(ds) < L0 && int64_t(de) - L0 > 128 + int64_t(b));
             if (k > 1 && __builtin_amdgcn_ballot_w64(!whole) == 0) {
                 if (phase == kData)
                     emit_whole_line(f, b, dw);
