@@ -33,22 +33,26 @@ constexpr uint32_t kSlot = 8192;          // one ring slot: 64 rows x one 128-by
 constexpr uint32_t kOOB = 0x80000000u;    // a voffset past every descriptor's range (DMA returns 0)
 constexpr uint32_t kRingWords = 64;       // funnel ring words per lane
 
-// LDS addresses of window dword j (0..32) of this lane for the window (k-1, k) with line k-1 in
-// slot 0 (ae) or slot 1 (ao).  Row `lane` of slot s holds the lane's line at granule positions
-// swizzled by swz(row) = (row >> 1) & 7 (applied on the DMA source side), so all 64 lanes reading
-// the same window dword hit different banks.
+// LDS addresses of window granule G (16 bytes, 0..8: dwords 4G .. 4G+3 of the window) of this lane
+// for the window (k-1, k) with line k-1 in slot 0 (ge) or slot 1 (go).  Row `lane` of slot s holds
+// the lane's line at granule positions swizzled by swz(row) = (row >> 1) & 7 (applied on the DMA
+// source side).  Every lane reads the same window granule at the same time (the window always
+// starts at its line's first byte), so the window is read with ds_read_b128: per 16-lane group the
+// granules sit in 16 distinct bank quads (rows alternate halves of the 64 banks, swz spreads the
+// eight positions), conflict-free -- with ds_read_b32 the 32 lanes of a group met on 8 banks
+// (4-way: 3.2 M conflict cycles per launch, round-4 PMC), and 33 reads became 9.
 struct Win {
-    uint32_t ae[33], ao[33];
+    uint32_t ge[9], go[9];
     uint32_t fr;                               // the lane's row in slot 0, OR its granule swizzle
     BRB_DEV void init(uint32_t slot0_lds, uint32_t lane)
     {
         fr = (slot0_lds + lane * 128) | (((lane >> 1) & 7) << 4);
 #pragma unroll
-        for (uint32_t j = 0; j < 33; j++) {
-            const uint32_t q4 = 4 * j;
-            ae[j] = ((q4 & 124u) ^ fr) + ((q4 & 128u) << 6);
-            ao[j] = ae[j] ^ kSlot;
-            asm volatile("" : "+v"(ao[j]));     // keep both tables (hipcc re-derived ao per use)
+        for (uint32_t G = 0; G < 9; G++) {
+            const uint32_t q4 = 16 * G;
+            ge[G] = ((q4 & 112u) ^ fr) + ((q4 & 128u) << 6);
+            go[G] = ge[G] ^ kSlot;
+            asm volatile("" : "+v"(go[G]));     // keep both tables
         }
     }
 };
@@ -62,13 +66,19 @@ BRB_DEV uint32_t win_dword(const Win &w, uint32_t j, uint32_t par)
     return lds_ld((((q4 & 124u) ^ w.fr) + ((q4 & 128u) << 6)) ^ (par ? kSlot : 0u));
 }
 
-// The 33 window dwords; returns once they are in registers (lgkmcnt(0)), so the slot of line k-1
-// may be refilled right after.
-BRB_DEV void read_window(const uint32_t (&ad)[33], uint32_t (&dw)[33])
+// The window's first 36 dwords (33 are used: line k-1 and line k's first dword); returns once they
+// are in registers (lgkmcnt(0)), so the slot of line k-1 may be refilled right after.
+BRB_DEV void read_window(const uint32_t (&ga)[9], uint32_t (&dw)[36])
 {
 #pragma unroll
-    for (int j = 0; j < 33; j++)
-        dw[j] = lds_ld(ad[j]);
+    for (int G = 0; G < 9; G++) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = *reinterpret_cast<const __attribute__((address_space(3))) v4u *>(ga[G]);
+        dw[4 * G + 0] = v.x;
+        dw[4 * G + 1] = v.y;
+        dw[4 * G + 2] = v.z;
+        dw[4 * G + 3] = v.w;
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);
 }
 
@@ -131,13 +141,13 @@ struct LineDesc {
 //   first  the range starts in this line, at byte ss (0..127); else it started in an earlier line
 //   endr   the range's end (exclusive), line-relative, > 0 (clamped: 4096 = "well past this line")
 //   b      the lane's word-grid phase inside lines (0..3), set here at the range's first line
-//   dw     the 33 window dwords
+//   dw     the window dwords (0..32 used)
 // Whole words go to the funnel ring; when the range's last word starts in this line, the bytes of a
 // last partial word become the carry and the call returns true (the range is done).  The caller adds
 // the range's length to f.total.
 template <uint32_t RW>
 BRB_DEV bool emit_range(brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32_t endr, uint32_t &b,
-                        const uint32_t (&dw)[33])
+                        const uint32_t (&dw)[36])
 {
     int o;                                                    // grid offset of the first word (-3..127)
     uint32_t e = 0;
@@ -182,7 +192,7 @@ BRB_DEV bool emit_range(brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32
 // The same for a staged segment line (md5_seg_kernels.hip): the range and the line in offsets from
 // the group's lowest line.
 template <uint32_t RW>
-BRB_DEV void emit_desc(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[33])
+BRB_DEV void emit_desc(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[36])
 {
     const bool first = d.ss >= d.line;
     if (first)
@@ -194,7 +204,7 @@ BRB_DEV void emit_desc(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, 
 // All 32 words of a line that lies wholly inside the lane's current range, not its first line
 // (the common case): no head, no bounds, no tail.
 template <uint32_t RW>
-BRB_DEV void emit_whole_line(brb_md5::FunnelT<RW> &f, uint32_t b, const uint32_t (&dw)[33])
+BRB_DEV void emit_whole_line(brb_md5::FunnelT<RW> &f, uint32_t b, const uint32_t (&dw)[36])
 {
     const uint32_t sh = 8 * b;
     const uint32_t wbase = f.lane4 + (f.wpos << 8);

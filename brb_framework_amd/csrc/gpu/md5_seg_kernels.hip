@@ -214,9 +214,9 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         issue_rows(rs, lds0, d0.line, lane);
         issue_rows(rs, lds0 + kSlot, d1.line, lane);
         uint32_t b = 0;
-        auto step = [&](uint32_t k, const uint32_t (&ad)[33], LineDesc &slot_d, uint32_t slot_lds) {
+        auto step = [&](uint32_t k, const uint32_t (&ad)[9], LineDesc &slot_d, uint32_t slot_lds) {
             brb_dma::wait_vmcnt<0>();
-            uint32_t dw[33];
+            uint32_t dw[36];
             read_window(ad, dw);
             const LineDesc d = slot_d;                  // line k-1
             if (k + 1 < K) {                            // line k+1 into the slot of line k-1
@@ -237,10 +237,10 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
             f.pump();
         };
         for (uint32_t k = 1; k <= K; k += 2) {
-            step(k, win.ae, d0, lds0);
+            step(k, win.ge, d0, lds0);
             if (k == K)
                 break;
-            step(k + 1, win.ao, d1, lds0 + kSlot);
+            step(k + 1, win.go, d1, lds0 + kSlot);
         }
         if (valid)
             store_digest(out, rec, f.finish());

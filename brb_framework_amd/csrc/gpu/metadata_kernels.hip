@@ -234,7 +234,7 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         // The walk's events whose first byte lies before pack byte L1, line k-1 = pack bytes [L0, L1)
         // in the window.  drain: after the last line, the events a pack shorter than its header
         // still reaches past its end (every byte there reads as 0: sz 0, no canary).
-        auto events = [&](int64_t L0, int64_t L1, uint32_t par, const uint32_t (&dw)[33], bool drain) {
+        auto events = [&](int64_t L0, int64_t L1, uint32_t par, const uint32_t (&dw)[36], bool drain) {
             auto rd32 = [&](int64_t p) -> uint32_t {           // pack bytes p .. p + 3, 0 past the pack
                 if (drain || uint64_t(p) >= size)
                     return 0u;
@@ -301,9 +301,9 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                 }
             }
         };
-        auto step = [&](uint32_t k, const uint32_t (&ad)[33], uint32_t par, uint32_t slot_lds) {
+        auto step = [&](uint32_t k, const uint32_t (&ad)[9], uint32_t par, uint32_t slot_lds) {
             brb_dma::wait_vmcnt<0>();
-            uint32_t dw[33];
+            uint32_t dw[36];
             read_window(ad, dw);
             // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
             const int64_t L0 = int64_t(128) * int64_t(k - 1) - int64_t(a0);
@@ -347,13 +347,13 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
             f.pump();
         };
         for (uint32_t k = 1; k <= K; k += 2) {
-            step(k, win.ae, 0, lds0);
+            step(k, win.ge, 0, lds0);
             if (k == K)
                 break;
-            step(k + 1, win.ao, 1, lds0 + kSlot);
+            step(k + 1, win.go, 1, lds0 + kSlot);
         }
         if (phase != kDone) {                                    // a pack shorter than its header
-            uint32_t dw[33] = {};
+            uint32_t dw[36] = {};
             events(int64_t(1) << 62, int64_t(1) << 62, 0, dw, true);
         }
         if (!valid)
