@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
+    ap.add_argument("--frame-stride", type=int, default=0,
+                    help="rc4md5: bytes from one frame's start to the next (default 1530 = back to back; 1536 "
+                         "puts every frame on a 64-byte sector boundary: the write-amplification experiment)")
     ap.add_argument("--len-dist", default="uniform", choices=["uniform", "bimodal"],
                     help="md5var / sha1var record lengths: U[1000, 2000] (default) or a bimodal diagnostic")
     ap.add_argument("--test-option", action="append", default=[], metavar="NAME=VALUE",
@@ -864,10 +867,12 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
     st0 = brb.rc4_states(keys)
     offs = torch.from_numpy(np.arange(n, dtype=np.uint64) * L).to(dev)
     lens = torch.full((n,), L, dtype=torch.int32, device=dev)
-    foffs = torch.from_numpy(np.arange(n, dtype=np.uint64) * (L + H)).to(dev)
+    FS = args.frame_stride or (L + H)
+    assert FS >= L + H, "--frame-stride below the frame size"
+    foffs = torch.from_numpy(np.arange(n, dtype=np.uint64) * FS).to(dev)
     flens = torch.full((n,), L + H, dtype=torch.int32, device=dev)
     salts = torch.from_numpy(rng.integers(0, 2**32, n, dtype=np.uint64)).to(dev)
-    frames = torch.zeros(n * (L + H), dtype=torch.uint8, device=dev)
+    frames = torch.zeros(n * FS, dtype=torch.uint8, device=dev)
     valid = torch.zeros(n, dtype=torch.uint8, device=dev)
     wst, rst = torch.from_numpy(st0).to(dev), torch.from_numpy(st0).to(dev)
     Lb = brb.lib()
@@ -911,6 +916,7 @@ def bench_rc4(args, rank, world, dev, stream, barrier, max_over_ranks, log):
         "data": f"synthetic (splitmix64 payloads, HBM-resident, {n_rot} rotating copies; random 16-byte keys)",
         "config": {"workload": f"f1: {n} connections x {L} B, 1 GPU" if world == 1 else f"f1: {n} connections/GPU",
                    "op": name + " (device mode)", "records_per_gpu": n, "record_bytes": L,
+                   "frame_stride": FS if args.op == "rc4md5" else None,
                    "parallelism": f"connection-shard x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": round(moved / step_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(moved / step_s / 1e9 / HBM_PEAK_GBS, 4),
