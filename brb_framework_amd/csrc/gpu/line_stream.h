@@ -30,56 +30,56 @@
 namespace brb_line {
 
 constexpr uint32_t kSlot = 8192;          // one ring slot: 64 rows x one 128-byte line
+constexpr uint32_t kSlots = 3;            // line j in slot j % 3: line k+1 lands during line k-1's work
 constexpr uint32_t kOOB = 0x80000000u;    // a voffset past every descriptor's range (DMA returns 0)
-constexpr uint32_t kRingWords = 64;       // funnel ring words per lane
+constexpr uint32_t kRingWords = 32;       // funnel ring words per lane (8 KiB per wave)
 
-// LDS addresses of window granule G (16 bytes, 0..8: dwords 4G .. 4G+3 of the window) of this lane
-// for the window (k-1, k) with line k-1 in slot 0 (ge) or slot 1 (go).  Row `lane` of slot s holds
-// the lane's line at granule positions swizzled by swz(row) = (row >> 1) & 7 (applied on the DMA
-// source side).  Every lane reads the same window granule at the same time (the window always
-// starts at its line's first byte), so the window is read with ds_read_b128: per 16-lane group the
-// granules sit in 16 distinct bank quads (rows alternate halves of the 64 banks, swz spreads the
-// eight positions), conflict-free -- with ds_read_b32 the 32 lanes of a group met on 8 banks
-// (4-way: 3.2 M conflict cycles per launch, round-4 PMC), and 33 reads became 9.
+// A lane's view of its rows in the ring.  Row `lane` of a slot holds the lane's line at granule
+// positions swizzled by swz(row) = (row >> 1) & 7 (applied on the DMA source side).  Every lane reads
+// the same window granule at the same time (the window always starts at its line's first byte), so
+// the window is read with ds_read_b128: per 16-lane group the granules sit in 16 distinct bank
+// quads (rows alternate halves of the 64 banks, swz spreads the eight positions), conflict-free --
+// with ds_read_b32 the 32 lanes of a group met on 8 banks (4-way: 3.2 M conflict cycles per launch,
+// round-4 PMC), and 33 reads became 9.
 struct Win {
-    uint32_t ge[9], go[9];
-    uint32_t fr;                               // the lane's row in slot 0, OR its granule swizzle
-    BRB_DEV void init(uint32_t slot0_lds, uint32_t lane)
+    uint32_t fr;                               // the lane's row offset in a slot, OR its granule swizzle
+    BRB_DEV void init(uint32_t lane)
     {
-        fr = (slot0_lds + lane * 128) | (((lane >> 1) & 7) << 4);
-#pragma unroll
-        for (uint32_t G = 0; G < 9; G++) {
-            const uint32_t q4 = 16 * G;
-            ge[G] = ((q4 & 112u) ^ fr) + ((q4 & 128u) << 6);
-            go[G] = ge[G] ^ kSlot;
-            asm volatile("" : "+v"(go[G]));     // keep both tables
-        }
+        fr = (lane * 128) | (((lane >> 1) & 7) << 4);
+    }
+    // window granule G (0..8) / dword j (0..63): line k-1 in the slot at LDS address sa, line k at sb
+    BRB_DEV uint32_t granule(uint32_t G, uint32_t sa, uint32_t sb) const
+    {
+        return (((16 * G) & 112u) ^ fr) + (G < 8 ? sa : sb);
+    }
+    BRB_DEV uint32_t dword_addr(uint32_t j, uint32_t sa, uint32_t sb) const
+    {
+        return (((4 * j) & 124u) ^ fr) + (j < 32 ? sa : sb);
     }
 };
 
 BRB_DEV uint32_t lds_ld(uint32_t a) { return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>(a); }
 
-// Window dword j (0..63) at a lane-varying j: line k-1 in slot `par`, line k in the other.
-BRB_DEV uint32_t win_dword(const Win &w, uint32_t j, uint32_t par)
-{
-    const uint32_t q4 = 4 * j;
-    return lds_ld((((q4 & 124u) ^ w.fr) + ((q4 & 128u) << 6)) ^ (par ? kSlot : 0u));
-}
-
 // The window's first 36 dwords (33 are used: line k-1 and line k's first dword); returns once they
 // are in registers (lgkmcnt(0)), so the slot of line k-1 may be refilled right after.
-BRB_DEV void read_window(const uint32_t (&ga)[9], uint32_t (&dw)[36])
+BRB_DEV void read_window(const Win &w, uint32_t sa, uint32_t sb, uint32_t (&dw)[36])
 {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int G = 0; G < 9; G++) {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u v = *reinterpret_cast<const __attribute__((address_space(3))) v4u *>(ga[G]);
+    for (uint32_t G = 0; G < 9; G++) {
+        const v4u v = *reinterpret_cast<const __attribute__((address_space(3))) v4u *>(w.granule(G, sa, sb));
         dw[4 * G + 0] = v.x;
         dw[4 * G + 1] = v.y;
         dw[4 * G + 2] = v.z;
         dw[4 * G + 3] = v.w;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
+}
+
+// Window dword j (0..63) at a lane-varying j.
+BRB_DEV uint32_t win_dword(const Win &w, uint32_t j, uint32_t sa, uint32_t sb)
+{
+    return lds_ld(w.dword_addr(j, sa, sb));
 }
 
 // Stage one line per row into the slot at LDS address `lm`: row r's line is `rel` of lane r
@@ -136,18 +136,24 @@ struct LineDesc {
     uint32_t line, ss, se;
 };
 
-// Emits the message words of one range that start in the window's line k-1 (see the file comment),
-// in line-relative byte coordinates:
+// The message words of one range that start in the window's line k-1 (see the file comment), in
+// line-relative byte coordinates:
 //   first  the range starts in this line, at byte ss (0..127); else it started in an earlier line
 //   endr   the range's end (exclusive), line-relative, > 0 (clamped: 4096 = "well past this line")
-//   b      the lane's word-grid phase inside lines (0..3), set here at the range's first line
-//   dw     the window dwords (0..32 used)
-// Whole words go to the funnel ring; when the range's last word starts in this line, the bytes of a
-// last partial word become the carry and the call returns true (the range is done).  The caller adds
-// the range's length to f.total.
+//   b      the lane's word-grid phase inside lines (0..3), set at the range's first line
+// Word i (-1..31) of the line's grid = window bytes b + 4i .. + 3; words i0 <= i < iw are whole and
+// go to ring position wpos0 + i - i0; when the range's last word starts in this line (ends), the
+// bytes of a last partial word (word it) become the carry.  Emitted in two halves (i < 16, i >= 16)
+// with the ring pumped between them, so a 32-word ring holds a line's words: before a half at most
+// 15 words wait, a half adds at most 17.
+struct Emit {
+    int i0, iw, it;
+    uint32_t sh, hmask, carry, rem, wbase, wpos0, tail;
+    bool ends, any;
+};
+
 template <uint32_t RW>
-BRB_DEV bool emit_range(brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32_t endr, uint32_t &b,
-                        const uint32_t (&dw)[36])
+BRB_DEV void plan_range(const brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32_t endr, uint32_t &b, Emit &p)
 {
     int o;                                                    // grid offset of the first word (-3..127)
     uint32_t e = 0;
@@ -158,61 +164,86 @@ BRB_DEV bool emit_range(brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, uint32
     } else {
         o = int(b);
     }
-    if (int(endr) <= o)                                       // its last word started in the line before
-        return true;
-    const int i0 = o >> 2;                                    // -1 .. 31
-    const int span = int(endr) - int(b);                      // > 4 i0
-    const int iw = span >> 2 < 32 ? span >> 2 : 32;           // whole words: i0 <= i < iw
-    const bool ends = span <= 128;                            // the range's last word starts here
-    const uint32_t rem = uint32_t(span) & 3u;                 // bytes of a last partial word
-    const int it = span >> 2;                                 // its index (when ends && rem)
-    const uint32_t sh = 8 * b;
-    const uint32_t carry = uint32_t(f.acc);
-    const uint32_t hmask = e ? (1u << (8 * e)) - 1u : 0u;
-    // word i goes to ring position wpos + i - i0
-    const uint32_t wbase = f.lane4 + ((f.wpos - uint32_t(i0)) << 8);
-    uint32_t tail = 0;
-#pragma unroll
-    for (int i = -1; i < 32; i++) {
-        uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], sh);
-        if (i == i0)
-            v = (v & ~hmask) | (carry & hmask);               // Funnel::head on the range's first word
-        if (i >= i0 && i < iw)
-            brb_md5::FunnelT<RW>::lds_st(((wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring, v);
-        tail = i == it ? v : tail;
+    p.any = int(endr) > o;                                    // else its last word started in the line before
+    p.i0 = o >> 2;                                            // -1 .. 31
+    const int span = int(endr) - int(b);                      // > 4 i0 when any
+    p.iw = span >> 2 < 32 ? span >> 2 : 32;                   // whole words: i0 <= i < iw
+    p.ends = p.any && span <= 128;                            // the range's last word starts here
+    p.rem = uint32_t(span) & 3u;                              // bytes of a last partial word
+    p.it = span >> 2;                                         // its index (when ends && rem)
+    p.sh = 8 * b;
+    p.carry = uint32_t(f.acc);
+    p.hmask = e ? (1u << (8 * e)) - 1u : 0u;
+    p.wpos0 = f.wpos;
+    p.wbase = f.lane4 + ((f.wpos - uint32_t(p.i0)) << 8);
+    p.tail = 0;
+    if (!p.any) {                                             // nothing to write
+        p.i0 = 0;
+        p.iw = 0;
+        p.it = -2;
     }
-    f.wpos += uint32_t(iw > i0 ? iw - i0 : 0);
-    if (ends) {
-        f.nacc = rem;
-        f.acc = rem ? (tail & ((1u << (8 * rem)) - 1u)) : 0u;
-    }
-    return ends;
 }
 
-// The same for a staged segment line (md5_seg_kernels.hip): the range and the line in offsets from
-// the group's lowest line.
+// A line wholly inside the lane's current range, not its first line and not the line of its last
+// word (the common case): 32 whole words, no head, no tail.
 template <uint32_t RW>
-BRB_DEV void emit_desc(brb_md5::FunnelT<RW> &f, const LineDesc &d, uint32_t &b, const uint32_t (&dw)[36])
+BRB_DEV void plan_whole(const brb_md5::FunnelT<RW> &f, uint32_t b, Emit &p)
 {
-    const bool first = d.ss >= d.line;
-    if (first)
-        f.total += d.se - d.ss;
-    const uint32_t endr = d.se - d.line < 4096u ? d.se - d.line : 4096u;
-    emit_range(f, first, d.ss - d.line, endr, b, dw);
+    p.any = true;
+    p.i0 = 0;
+    p.iw = 32;
+    p.it = -2;
+    p.ends = false;
+    p.rem = 0;
+    p.sh = 8 * b;
+    p.carry = 0;
+    p.hmask = 0;
+    p.wpos0 = f.wpos;
+    p.wbase = f.lane4 + (f.wpos << 8);
+    p.tail = 0;
 }
 
-// All 32 words of a line that lies wholly inside the lane's current range, not its first line
-// (the common case): no head, no bounds, no tail.
-template <uint32_t RW>
-BRB_DEV void emit_whole_line(brb_md5::FunnelT<RW> &f, uint32_t b, const uint32_t (&dw)[36])
+template <uint32_t RW, int H, bool WHOLE>
+BRB_DEV void emit_half(brb_md5::FunnelT<RW> &f, Emit &p, const uint32_t (&dw)[36])
 {
-    const uint32_t sh = 8 * b;
-    const uint32_t wbase = f.lane4 + (f.wpos << 8);
+    constexpr int lo = H ? 16 : -1, hi = H ? 32 : 16;
 #pragma unroll
-    for (int i = 0; i < 32; i++)
-        brb_md5::FunnelT<RW>::lds_st(((wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring,
-                                     __builtin_amdgcn_alignbit(dw[i + 1], dw[i], sh));
-    f.wpos += 32;
+    for (int i = lo; i < hi; i++) {
+        if (WHOLE && i < 0)
+            continue;
+        uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], p.sh);
+        const uint32_t a = ((p.wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring;
+        if (WHOLE) {
+            brb_md5::FunnelT<RW>::lds_st(a, v);
+        } else {
+            if (i == p.i0)
+                v = (v & ~p.hmask) | (p.carry & p.hmask);     // Funnel::head on the range's first word
+            if (i >= p.i0 && i < p.iw)
+                brb_md5::FunnelT<RW>::lds_st(a, v);
+            p.tail = i == p.it ? v : p.tail;
+        }
+    }
+    // words written so far: [i0, min(iw, hi))
+    const int top = p.iw < hi ? p.iw : hi;
+    f.wpos = p.wpos0 + uint32_t(top > p.i0 ? top - p.i0 : 0);
+}
+
+template <uint32_t RW>
+BRB_DEV void emit_finish(brb_md5::FunnelT<RW> &f, const Emit &p)
+{
+    if (p.ends) {
+        f.nacc = p.rem;
+        f.acc = p.rem ? (p.tail & ((1u << (8 * p.rem)) - 1u)) : 0u;
+    }
+}
+
+// Compresses every whole block waiting in the ring (one compress site per call; at most two blocks
+// wait after a half).
+template <uint32_t RW>
+BRB_DEV void pump_all(brb_md5::FunnelT<RW> &f)
+{
+    while (f.wpos - f.cpos >= 16)
+        f.pump();
 }
 
 }  // namespace brb_line

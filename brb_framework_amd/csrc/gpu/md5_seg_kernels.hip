@@ -106,11 +106,12 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
 }
 
 // Line-staged kernel (round 4; line_stream.h).  A wave digests groups of 64 records, one per lane;
-// a lane's VIRTUAL lines are its non-empty segments' 128-byte memory lines in order, staged two
-// ahead by LDS-DMA into a two-slot ring.  Per line: the 33-dword window, the next stage issued, the
-// segment's words that start in this line emitted into the lane's 64-word funnel ring, and up to
-// three 16-word blocks compressed.  W waves per workgroup, W * 38 KiB of LDS; groups strided over
-// the grid.
+// a lane's VIRTUAL lines are its non-empty segments' 128-byte memory lines in order, staged by
+// LDS-DMA into a three-slot ring: at iteration k the window is lines (k-1, k), line k+1 is in flight
+// since iteration k-1, and line k+2 goes into line k-1's slot once the window is read.  The
+// segment's words that start in line k-1 go to the lane's 32-word funnel ring in two halves, whole
+// blocks compressed after each.  W waves per workgroup, W * 38 KiB of LDS; groups strided over the
+// grid.
 template <int W>
 __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__restrict__ data,
                                                                const uint64_t *__restrict__ soff,
@@ -121,17 +122,17 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
     using namespace brb_line;
     constexpr uint32_t RW = brb_line::kRingWords;
     constexpr uint32_t kTab = 512;                      // segments per group held in LDS (8 per record)
-    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * 2 * kSlot];
-    __shared__ __attribute__((aligned(16384))) uint32_t fring[W][RW][64];
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * kSlots * kSlot];
+    __shared__ __attribute__((aligned(8192))) uint32_t fring[W][RW][64];
     __shared__ uint64_t tab_off[W][kTab];
     __shared__ uint32_t tab_len[W][kTab];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * 2 * kSlot;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * kSlots * kSlot;
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
     Win win;
-    win.init(lds0, lane);
+    win.init(lane);
 
     for (uint64_t g = uint64_t(blockIdx.x) * W + wv; g < n_groups; g += uint64_t(gridDim.x) * W) {
         const uint64_t rec = g * 64 + lane;
@@ -209,39 +210,61 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 c_line = c_line == c_last ? kEnd : c_line + 128;
             return d;
         };
-        LineDesc d0 = stage_line();                             // the lines in slots 0 and 1
-        LineDesc d1 = stage_line();
-        issue_rows(rs, lds0, d0.line, lane);
-        issue_rows(rs, lds0 + kSlot, d1.line, lane);
+        // lines 0, 1, 2 -> slots 0, 1, 2; dA / dB / dC: the lines k-1, k, k+1 at iteration k
+        LineDesc dA = stage_line(), dB = stage_line(), dC = stage_line();
+        issue_rows(rs, lds0, dA.line, lane);
+        issue_rows(rs, lds0 + kSlot, dB.line, lane);
+        issue_rows(rs, lds0 + 2 * kSlot, dC.line, lane);
         uint32_t b = 0;
-        auto step = [&](uint32_t k, const uint32_t (&ad)[9], LineDesc &slot_d, uint32_t slot_lds) {
-            brb_dma::wait_vmcnt<0>();
+        uint32_t sa = 0;                                // byte offset of line k-1's slot (uniform)
+        for (uint32_t k = 1; k <= K; k++) {
+            const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;   // line k's slot
+            brb_dma::wait_vmcnt<8>();                   // line k landed; line k+1's 8 DMAs may fly
             uint32_t dw[36];
-            read_window(ad, dw);
-            const LineDesc d = slot_d;                  // line k-1
-            if (k + 1 < K) {                            // line k+1 into the slot of line k-1
-                slot_d = stage_line();
-                issue_rows(rs, slot_lds, slot_d.line, lane);
+            read_window(win, lds0 + sa, lds0 + sb, dw);
+            const LineDesc d = dA;                      // line k-1
+            dA = dB;
+            dB = dC;
+            dC = stage_line();                          // line k+2 into line k-1's slot (kOOB rows past the end)
+            issue_rows(rs, lds0 + sa, dC.line, lane);
+            const bool has = d.line != kOOB;
+            // whole line inside the segment, and not the line of its last word (the carry is set there)
+            const bool whole = has && d.ss < d.line && d.se - d.line > 128u + b;
+            const bool all_whole = __builtin_amdgcn_ballot_w64(has && !whole) == 0;
+            Emit e;
+            if (all_whole) {
+                plan_whole(f, b, e);
+            } else {
+                const bool fst = d.ss >= d.line;
+                if (has && fst)
+                    f.total += d.se - d.ss;
+                plan_range(f, fst, d.ss - d.line, d.se - d.line < 4096u ? d.se - d.line : 4096u, b, e);
             }
-            if (d.line != kOOB) {
-                // whole line inside the segment, and not the line of its last word (emit_range sets
-                // the carry there)
-                const bool whole = d.ss < d.line && d.se - d.line > 128u + b;
-                if (__builtin_amdgcn_ballot_w64(d.line != kOOB && !whole) == 0)
-                    emit_whole_line(f, b, dw);
+            if (!has) {                                 // no line for this lane: nothing to write
+                e.any = false;
+                e.ends = false;
+                e.i0 = 0;
+                e.iw = 0;
+                e.it = -2;
+            }
+            if (has) {
+                if (all_whole)
+                    emit_half<RW, 0, true>(f, e, dw);
                 else
-                    emit_desc(f, d, b, dw);
+                    emit_half<RW, 0, false>(f, e, dw);
             }
-            f.pump();
-            f.pump();
-            f.pump();
-        };
-        for (uint32_t k = 1; k <= K; k += 2) {
-            step(k, win.ge, d0, lds0);
-            if (k == K)
-                break;
-            step(k + 1, win.go, d1, lds0 + kSlot);
+            pump_all(f);
+            if (has) {
+                if (all_whole)
+                    emit_half<RW, 1, true>(f, e, dw);
+                else
+                    emit_half<RW, 1, false>(f, e, dw);
+                emit_finish(f, e);
+            }
+            pump_all(f);
+            sa = sb;
         }
+        brb_dma::wait_vmcnt<0>();                       // the stray stages past K, before the slots are reused
         if (valid)
             store_digest(out, rec, f.finish());
     }

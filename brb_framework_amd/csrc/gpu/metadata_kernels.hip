@@ -180,8 +180,9 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
 //                        -> CANARY once its last word is out
 //   CANARY at de:        the 0x1F check, items++, offset == size stops the walk, -> FIELDS
 // Every event is handled in the line that holds its first byte, so the window always holds what it
-// reads; the whole line's reads happen before that line's slot is refilled.  Per line up to 33
-// words go to the ring and up to three blocks are compressed.  The return codes and the unsigned
+// reads; the whole line's reads happen before that line's slot is refilled.  Three ring slots: line
+// k+1 is in flight during line k-1's work.  An item's words go to the lane's 32-word funnel ring in
+// two halves per line, whole blocks compressed after each.  The return codes and the unsigned
 // long arithmetic of cur_offset / cur_remaining / cur_needed are unpack_lane's (the reference's).
 template <int W>
 __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__restrict__ data,
@@ -192,15 +193,15 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
     using namespace brb_line;
     constexpr uint32_t RW = brb_line::kRingWords;
     enum : uint32_t { kFields = 0, kData = 1, kCanary = 2, kDone = 3 };
-    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * 2 * kSlot];
-    __shared__ __attribute__((aligned(16384))) uint32_t fring[W][RW][64];
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * kSlots * kSlot];
+    __shared__ __attribute__((aligned(8192))) uint32_t fring[W][RW][64];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n + 63) / 64;
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * 2 * kSlot;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * kSlots * kSlot;
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
     Win win;
-    win.init(lds0, lane);
+    win.init(lane);
 
     for (uint64_t g = uint64_t(blockIdx.x) * W + wv; g < n_groups; g += uint64_t(gridDim.x) * W) {
         const uint64_t r = g * 64 + lane;
@@ -226,6 +227,7 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         auto line_rel = [&](uint32_t j) { return j < nl ? rel0 + 128 * j : kOOB; };
         issue_rows(rs, lds0, line_rel(0), lane);
         issue_rows(rs, lds0 + kSlot, line_rel(1), lane);
+        issue_rows(rs, lds0 + 2 * kSlot, line_rel(2), lane);
 
         int32_t code = BRB_METADATA_UNPACK_SUCCESS, item_count = 0, item = 0;
         uint32_t items = 0, phase = kDone, b = 0, dig[4] = {0, 0, 0, 0};
@@ -234,13 +236,13 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         // The walk's events whose first byte lies before pack byte L1, line k-1 = pack bytes [L0, L1)
         // in the window.  drain: after the last line, the events a pack shorter than its header
         // still reaches past its end (every byte there reads as 0: sz 0, no canary).
-        auto events = [&](int64_t L0, int64_t L1, uint32_t par, const uint32_t (&dw)[36], bool drain) {
+        auto events = [&](int64_t L0, int64_t L1, uint32_t sa, uint32_t sb, const uint32_t (&dw)[36], bool drain) {
             auto rd32 = [&](int64_t p) -> uint32_t {           // pack bytes p .. p + 3, 0 past the pack
                 if (drain || uint64_t(p) >= size)
                     return 0u;
                 const uint32_t wb = uint32_t(p - L0);
-                const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, par),
-                                                             win_dword(win, wb >> 2, par), 8 * (wb & 3));
+                const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, sa, sb),
+                                                             win_dword(win, wb >> 2, sa, sb), 8 * (wb & 3));
                 const uint64_t left = size - uint64_t(p);
                 return left >= 4 ? v : v & ((1u << (8 * uint32_t(left))) - 1u);
             };
@@ -280,8 +282,17 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                 if (phase == kData && int64_t(ds) < L1) {        // :249-254 BRB_MD5UpdateBig of the data
                     const bool first = int64_t(ds) >= L0;
                     const int64_t er = int64_t(de) - L0;
-                    const bool done = de == ds || drain ||
-                                      emit_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, dw);
+                    bool done = de == ds || drain;
+                    if (!done) {
+                        Emit e;
+                        plan_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, e);
+                        emit_half<RW, 0, false>(f, e, dw);
+                        pump_all(f);
+                        emit_half<RW, 1, false>(f, e, dw);
+                        emit_finish(f, e);
+                        pump_all(f);
+                        done = !e.any || e.ends;
+                    }
                     more = done;                                 // else the line is used up (no second emission)
                     if (done)
                         phase = kCanary;
@@ -301,10 +312,12 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                 }
             }
         };
-        auto step = [&](uint32_t k, const uint32_t (&ad)[9], uint32_t par, uint32_t slot_lds) {
-            brb_dma::wait_vmcnt<0>();
+        uint32_t sa = 0;                                         // byte offset of line k-1's slot (uniform)
+        for (uint32_t k = 1; k <= K; k++) {
+            const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;  // line k's slot
+            brb_dma::wait_vmcnt<8>();                            // line k landed; line k+1 may fly
             uint32_t dw[36];
-            read_window(ad, dw);
+            read_window(win, lds0 + sa, lds0 + sb, dw);
             // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
             const int64_t L0 = int64_t(128) * int64_t(k - 1) - int64_t(a0);
             if (k == 1 && valid) {                               // MetaDataHeader (libbrb_data.h:322-330)
@@ -312,8 +325,8 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                     if (p >= size)
                         return 0u;
                     const uint32_t wb = p + a0;
-                    const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, par),
-                                                                 win_dword(win, wb >> 2, par), 8 * (wb & 3));
+                    const uint32_t v = __builtin_amdgcn_alignbit(win_dword(win, (wb >> 2) + 1, lds0 + sa, lds0 + sb),
+                                                                 win_dword(win, wb >> 2, lds0 + sa, lds0 + sb), 8 * (wb & 3));
                     const uint64_t left = size - p;
                     return left >= 4 ? v : v & ((1u << (8 * uint32_t(left))) - 1u);
                 };
@@ -331,30 +344,29 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
             }
             // the common line: every walking lane is inside an item's data that covers the whole
             // line and goes on past its 32 words (not its first line, not the line of its last word,
-            // which emit_range must see to set the carry) -> 32 whole words, no event to look for
+            // where the carry is set) -> 32 whole words, no event to look for
             const bool whole = phase == kDone ||
                                (phase == kData && int64_t(ds) < L0 && int64_t(de) - L0 > 128 + int64_t(b));
             if (k > 1 && __builtin_amdgcn_ballot_w64(!whole) == 0) {
+                Emit e;
+                plan_whole(f, b, e);
                 if (phase == kData)
-                    emit_whole_line(f, b, dw);
+                    emit_half<RW, 0, true>(f, e, dw);
+                pump_all(f);
+                if (phase == kData)
+                    emit_half<RW, 1, true>(f, e, dw);
+                pump_all(f);
             } else {
-                events(L0, L0 + 128, par, dw, false);
+                events(L0, L0 + 128, lds0 + sa, lds0 + sb, dw, false);
             }
-            if (k + 1 < K)                                       // line k+1 into the slot of line k-1
-                issue_rows(rs, slot_lds, phase == kDone ? kOOB : line_rel(k + 1), lane);
-            f.pump();
-            f.pump();
-            f.pump();
-        };
-        for (uint32_t k = 1; k <= K; k += 2) {
-            step(k, win.ge, 0, lds0);
-            if (k == K)
-                break;
-            step(k + 1, win.go, 1, lds0 + kSlot);
+            // line k+2 into line k-1's slot (its window reads are done)
+            issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + 2), lane);
+            sa = sb;
         }
+        brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
         if (phase != kDone) {                                    // a pack shorter than its header
             uint32_t dw[36] = {};
-            events(int64_t(1) << 62, int64_t(1) << 62, 0, dw, true);
+            events(int64_t(1) << 62, int64_t(1) << 62, 0, 0, dw, true);
         }
         if (!valid)
             continue;
