@@ -217,16 +217,27 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         issue_rows(rs, lds0 + 2 * kSlot, dC.line, lane);
         uint32_t b = 0;
         uint32_t sa = 0;                                // byte offset of line k-1's slot (uniform)
+#ifdef BRB_LINE_STAMPS    // diagnostic builds only (make -C brb_framework_amd diag; tools/seg_probe.py)
+        uint64_t acc_wait = 0, acc_win = 0, acc_stage = 0, acc_emit = 0, acc_pump = 0;
+        const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#define BRB_STAMP(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define BRB_STAMP(v)
+#endif
         for (uint32_t k = 1; k <= K; k++) {
             const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;   // line k's slot
+            BRB_STAMP(t0);
             brb_dma::wait_vmcnt<8>();                   // line k landed; line k+1's 8 DMAs may fly
+            BRB_STAMP(t1);
             uint32_t dw[36];
             read_window(win, lds0 + sa, lds0 + sb, dw);
+            BRB_STAMP(t2);
             const LineDesc d = dA;                      // line k-1
             dA = dB;
             dB = dC;
             dC = stage_line();                          // line k+2 into line k-1's slot (kOOB rows past the end)
             issue_rows(rs, lds0 + sa, dC.line, lane);
+            BRB_STAMP(t3);
             const bool has = d.line != kOOB;
             // whole line inside the segment, and not the line of its last word (the carry is set there)
             const bool whole = has && d.ss < d.line && d.se - d.line > 128u + b;
@@ -253,7 +264,9 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 else
                     emit_half<RW, 0, false>(f, e, dw);
             }
+            BRB_STAMP(t4);
             pump_all(f);
+            BRB_STAMP(t5);
             if (has) {
                 if (all_whole)
                     emit_half<RW, 1, true>(f, e, dw);
@@ -261,10 +274,29 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                     emit_half<RW, 1, false>(f, e, dw);
                 emit_finish(f, e);
             }
+            BRB_STAMP(t6);
             pump_all(f);
+            BRB_STAMP(t7);
+#ifdef BRB_LINE_STAMPS
+            acc_wait += t1 - t0;
+            acc_win += t2 - t1;
+            acc_stage += t3 - t2;
+            acc_emit += (t4 - t3) + (t6 - t5);
+            acc_pump += (t5 - t4) + (t7 - t6);
+#endif
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                       // the stray stages past K, before the slots are reused
+#ifdef BRB_LINE_STAMPS
+        // lane 0's digest slot: wait, window, stage, emit; lane 1's: pump, total, K, 0 (cycles)
+        const uint64_t t_end = __builtin_amdgcn_s_memtime();
+        if (lane < 2 && valid) {
+            const uint4 v = lane == 0 ? make_uint4(uint32_t(acc_wait), uint32_t(acc_win), uint32_t(acc_stage), uint32_t(acc_emit))
+                                      : make_uint4(uint32_t(acc_pump), uint32_t(t_end - t_start), K, 0u);
+            __builtin_memcpy(out + 16 * rec, &v, 16);
+        }
+        continue;
+#endif
         if (valid)
             store_digest(out, rec, f.finish());
     }
