@@ -86,16 +86,27 @@ BRB_DEV uint32_t win_dword(const Win &w, uint32_t j, uint32_t sa, uint32_t sb)
 // (its offset from the group's lowest line, a multiple of 128), or kOOB for none.  DMA lane
 // (q, l3 = lane >> 3) moves granule (lane & 7) ^ swz(row) of row 8q + l3's line; the descriptor's
 // base is 4 KiB below the lowest line and four DMAs share one M0 through their instruction offsets.
-BRB_DEV void issue_rows(const brb_dma::v4i &rs, uint32_t lm, uint32_t rel, uint32_t lane)
+// prep_rows gathers the rows' offsets (8 ds_bpermute) -- early, so their LDS round trip overlaps
+// the wait for the current line; fire_rows issues the DMAs.
+struct RowsV {
+    uint32_t v[8];
+};
+
+BRB_DEV RowsV prep_rows(uint32_t rel, uint32_t lane)
 {
     const uint32_t l3 = lane >> 3;
     const uint32_t g0 = 16u * ((lane & 7) ^ (l3 >> 1));   // swz(8q + l3) = (l3 >> 1) ^ 4 (q & 1)
-    uint32_t v[8];
+    RowsV r;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const uint32_t rr = uint32_t(__builtin_amdgcn_ds_bpermute(int(8 * q + l3) * 4, int(rel)));
-        v[q] = rr >= kOOB ? kOOB : (rr | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
+        r.v[q] = rr >= kOOB ? kOOB : (rr | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
     }
+    return r;
+}
+
+BRB_DEV void fire_rows(const brb_dma::v4i &rs, uint32_t lm, const RowsV &r)
+{
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\t"
                  "s_mov_b32 m0, %10\n\t"
@@ -112,9 +123,14 @@ BRB_DEV void issue_rows(const brb_dma::v4i &rs, uint32_t lm, uint32_t rel, uint3
                  "buffer_load_dwordx4 %8, %9, 0 offen offset:3072 nt lds\n\t"
                  "s_mov_b32 m0, %0"
                  : "=&s"(keep)
-                 : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
-                   "s"(rs), "s"(lm), "s"(lm + 4096u)
+                 : "v"(r.v[0]), "v"(r.v[1]), "v"(r.v[2]), "v"(r.v[3]), "v"(r.v[4]), "v"(r.v[5]), "v"(r.v[6]),
+                   "v"(r.v[7]), "s"(rs), "s"(lm), "s"(lm + 4096u)
                  : "memory");
+}
+
+BRB_DEV void issue_rows(const brb_dma::v4i &rs, uint32_t lm, uint32_t rel, uint32_t lane)
+{
+    fire_rows(rs, lm, prep_rows(rel, lane));
 }
 
 // Descriptor for a group whose lines lie in [lo, hi) (128-byte aligned absolute addresses).
@@ -146,9 +162,16 @@ struct LineDesc {
 // bytes of a last partial word (word it) become the carry.  Emitted in two halves (i < 16, i >= 16)
 // with the ring pumped between them, so a 32-word ring holds a line's words: before a half at most
 // 15 words wait, a half adds at most 17.
+// Every word of a half is written, unconditionally: a word before i0 to slot wpos0 (word i0
+// overwrites it later in program order), a word past the range to the first slot after the half's
+// words (free, and never one still waiting: a half that fills the ring has no such word) -- one
+// v_med3 on the address instead of a branch per word.  The first word's carried bytes (head) and
+// the last partial word (tail) are built once, from the two window dwords each reads back by
+// address (edge_words) before the line's slot is refilled.
 struct Emit {
     int i0, iw, it;
-    uint32_t sh, hmask, carry, rem, wbase, wpos0, tail;
+    uint32_t sh, hmask, carry, rem, wpos0, abase, alo;
+    uint32_t head, tail;            // word i0 with the carried bytes in, word it (raw)
     bool ends, any;
 };
 
@@ -175,13 +198,29 @@ BRB_DEV void plan_range(const brb_md5::FunnelT<RW> &f, bool first, uint32_t ss, 
     p.carry = uint32_t(f.acc);
     p.hmask = e ? (1u << (8 * e)) - 1u : 0u;
     p.wpos0 = f.wpos;
-    p.wbase = f.lane4 + ((f.wpos - uint32_t(p.i0)) << 8);
-    p.tail = 0;
     if (!p.any) {                                             // nothing to write
         p.i0 = 0;
         p.iw = 0;
         p.it = -2;
     }
+    p.abase = f.lane4 + ((f.wpos - uint32_t(p.i0)) << 8);
+    p.alo = f.lane4 + (f.wpos << 8);
+    p.head = 0;
+    p.tail = 0;
+}
+
+// Words i0 and it of a planned range, from the window dwords by address (line k-1 at sa, line k at
+// sb), before the slot of line k-1 is refilled.
+BRB_DEV void edge_words(const Win &w, uint32_t sa, uint32_t sb, Emit &p)
+{
+    const uint32_t j0 = p.i0 < 0 ? 0u : uint32_t(p.i0);       // i0 = -1: the dword below the line holds
+    const uint32_t jt = p.it < 0 ? 0u : p.it > 31 ? 31u : uint32_t(p.it);   // only carried bytes
+    const uint32_t h1 = win_dword(w, uint32_t(p.i0 + 1), sa, sb);
+    const uint32_t h0 = p.i0 < 0 ? h1 : win_dword(w, j0, sa, sb);
+    const uint32_t t0 = win_dword(w, jt, sa, sb), t1 = win_dword(w, jt + 1, sa, sb);
+    const uint32_t raw = __builtin_amdgcn_alignbit(h1, h0, p.sh);
+    p.head = (raw & ~p.hmask) | (p.carry & p.hmask);
+    p.tail = p.it == p.i0 ? p.head : __builtin_amdgcn_alignbit(t1, t0, p.sh);
 }
 
 // A line wholly inside the lane's current range, not its first line and not the line of its last
@@ -199,7 +238,9 @@ BRB_DEV void plan_whole(const brb_md5::FunnelT<RW> &f, uint32_t b, Emit &p)
     p.carry = 0;
     p.hmask = 0;
     p.wpos0 = f.wpos;
-    p.wbase = f.lane4 + (f.wpos << 8);
+    p.abase = f.lane4 + (f.wpos << 8);
+    p.alo = p.abase;
+    p.head = 0;
     p.tail = 0;
 }
 
@@ -207,25 +248,24 @@ template <uint32_t RW, int H, bool WHOLE>
 BRB_DEV void emit_half(brb_md5::FunnelT<RW> &f, Emit &p, const uint32_t (&dw)[36])
 {
     constexpr int lo = H ? 16 : -1, hi = H ? 32 : 16;
+    constexpr uint32_t M = brb_md5::FunnelT<RW>::kMask;
+    // words written after this half: [i0, min(iw, hi)); the first slot after them
+    const int top = p.iw < hi ? p.iw : hi;
+    const uint32_t n = uint32_t(top > p.i0 ? top - p.i0 : 0);
+    const uint32_t ahi = p.alo + (n << 8);
 #pragma unroll
     for (int i = lo; i < hi; i++) {
         if (WHOLE && i < 0)
             continue;
-        uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], p.sh);
-        const uint32_t a = ((p.wbase + uint32_t(i << 8)) & brb_md5::FunnelT<RW>::kMask) | f.ring;
-        if (WHOLE) {
-            brb_md5::FunnelT<RW>::lds_st(a, v);
-        } else {
-            if (i == p.i0)
-                v = (v & ~p.hmask) | (p.carry & p.hmask);     // Funnel::head on the range's first word
-            if (i >= p.i0 && i < p.iw)
-                brb_md5::FunnelT<RW>::lds_st(a, v);
-            p.tail = i == p.it ? v : p.tail;
-        }
+        const uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], p.sh);
+        uint32_t a = p.abase + uint32_t(i << 8);
+        if (!WHOLE)
+            asm("v_med3_u32 %0, %1, %2, %3" : "=v"(a) : "v"(a), "v"(p.alo), "v"(ahi));   // before i0 -> wpos0, past the range -> free slot (alo <= ahi)
+        brb_md5::FunnelT<RW>::lds_st((a & M) | f.ring, v);
     }
-    // words written so far: [i0, min(iw, hi))
-    const int top = p.iw < hi ? p.iw : hi;
-    f.wpos = p.wpos0 + uint32_t(top > p.i0 ? top - p.i0 : 0);
+    if (!WHOLE && p.hmask && p.i0 >= lo && p.i0 < hi && p.i0 < p.iw)   // the head, over word i0's slot
+        brb_md5::FunnelT<RW>::lds_st((p.alo & M) | f.ring, p.head);
+    f.wpos = p.wpos0 + n;
 }
 
 template <uint32_t RW>

@@ -227,6 +227,8 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         for (uint32_t k = 1; k <= K; k++) {
             const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;   // line k's slot
             BRB_STAMP(t0);
+            const LineDesc dn = stage_line();           // line k+2 (kOOB rows past the end): its rows'
+            const RowsV rv = prep_rows(dn.line, lane);  // offsets gathered while line k lands
             brb_dma::wait_vmcnt<8>();                   // line k landed; line k+1's 8 DMAs may fly
             BRB_STAMP(t1);
             uint32_t dw[36];
@@ -235,9 +237,7 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
             const LineDesc d = dA;                      // line k-1
             dA = dB;
             dB = dC;
-            dC = stage_line();                          // line k+2 into line k-1's slot (kOOB rows past the end)
-            issue_rows(rs, lds0 + sa, dC.line, lane);
-            BRB_STAMP(t3);
+            dC = dn;
             const bool has = d.line != kOOB;
             // whole line inside the segment, and not the line of its last word (the carry is set there)
             const bool whole = has && d.ss < d.line && d.se - d.line > 128u + b;
@@ -250,7 +250,12 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 if (has && fst)
                     f.total += d.se - d.ss;
                 plan_range(f, fst, d.ss - d.line, d.se - d.line < 4096u ? d.se - d.line : 4096u, b, e);
+                if (has)
+                    edge_words(win, lds0 + sa, lds0 + sb, e);
+                __builtin_amdgcn_s_waitcnt(0xC07F);     // those reads are in before the slot is refilled
             }
+            fire_rows(rs, lds0 + sa, rv);               // line k+2 into line k-1's slot
+            BRB_STAMP(t3);
             if (!has) {                                 // no line for this lane: nothing to write
                 e.any = false;
                 e.ends = false;

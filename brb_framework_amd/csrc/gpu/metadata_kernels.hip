@@ -286,6 +286,7 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                     if (!done) {
                         Emit e;
                         plan_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, e);
+                        edge_words(win, sa, sb, e);
                         emit_half<RW, 0, false>(f, e, dw);
                         pump_all(f);
                         emit_half<RW, 1, false>(f, e, dw);
