@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
 // segment's words that start in line k-1 go to the lane's 32-word funnel ring in two halves, whole
 // blocks compressed after each.  W waves per workgroup, W * 38 KiB of LDS; groups strided over the
 // grid.
-template <int W>
+template <int W, int NS>
 __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__restrict__ data,
                                                                const uint64_t *__restrict__ soff,
                                                                const uint32_t *__restrict__ slen,
@@ -122,14 +122,15 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
     using namespace brb_line;
     constexpr uint32_t RW = brb_line::kRingWords;
     constexpr uint32_t kTab = 512;                      // segments per group held in LDS (8 per record)
-    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * kSlots * kSlot];
+    static_assert(NS == 2 || NS == 3, "two or three ring slots");
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * NS * kSlot];
     __shared__ __attribute__((aligned(8192))) uint32_t fring[W][RW][64];
     __shared__ uint64_t tab_off[W][kTab];
     __shared__ uint32_t tab_len[W][kTab];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * kSlots * kSlot;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * NS * kSlot;
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
     Win win;
     win.init(lane);
@@ -210,11 +211,14 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                 c_line = c_line == c_last ? kEnd : c_line + 128;
             return d;
         };
-        // lines 0, 1, 2 -> slots 0, 1, 2; dA / dB / dC: the lines k-1, k, k+1 at iteration k
-        LineDesc dA = stage_line(), dB = stage_line(), dC = stage_line();
+        // lines 0 .. NS-1 -> slots 0 .. NS-1; dA, dB (, dC): the lines k-1, k (, k+1) at iteration k
+        LineDesc dA = stage_line(), dB = stage_line(), dC = dB;
         issue_rows(rs, lds0, dA.line, lane);
         issue_rows(rs, lds0 + kSlot, dB.line, lane);
-        issue_rows(rs, lds0 + 2 * kSlot, dC.line, lane);
+        if (NS == 3) {
+            dC = stage_line();
+            issue_rows(rs, lds0 + 2 * kSlot, dC.line, lane);
+        }
         uint32_t b = 0;
         uint32_t sa = 0;                                // byte offset of line k-1's slot (uniform)
 #ifdef BRB_LINE_STAMPS    // diagnostic builds only (make -C brb_framework_amd diag; tools/seg_probe.py)
@@ -225,19 +229,23 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
 #define BRB_STAMP(v)
 #endif
         for (uint32_t k = 1; k <= K; k++) {
-            const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;   // line k's slot
+            const uint32_t sb = sa == (NS - 1) * kSlot ? 0u : sa + kSlot;   // line k's slot
             BRB_STAMP(t0);
-            const LineDesc dn = stage_line();           // line k+2 (kOOB rows past the end): its rows'
-            const RowsV rv = prep_rows(dn.line, lane);  // offsets gathered while line k lands
-            brb_dma::wait_vmcnt<8>();                   // line k landed; line k+1's 8 DMAs may fly
+            const LineDesc dn = stage_line();           // line k+NS-1 (kOOB rows past the end): its
+            const RowsV rv = prep_rows(dn.line, lane);  // rows' offsets gathered while line k lands
+            brb_dma::wait_vmcnt<NS == 3 ? 8 : 0>();     // line k landed (NS = 3: line k+1's 8 DMAs may fly)
             BRB_STAMP(t1);
             uint32_t dw[36];
             read_window(win, lds0 + sa, lds0 + sb, dw);
             BRB_STAMP(t2);
             const LineDesc d = dA;                      // line k-1
             dA = dB;
-            dB = dC;
-            dC = dn;
+            if (NS == 3) {
+                dB = dC;
+                dC = dn;
+            } else {
+                dB = dn;
+            }
             const bool has = d.line != kOOB;
             // whole line inside the segment, and not the line of its last word (the carry is set there)
             const bool whole = has && d.ss < d.line && d.se - d.line > 128u + b;
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
                     edge_words(win, lds0 + sa, lds0 + sb, e);
                 __builtin_amdgcn_s_waitcnt(0xC07F);     // those reads are in before the slot is refilled
             }
-            fire_rows(rs, lds0 + sa, rv);               // line k+2 into line k-1's slot
+            fire_rows(rs, lds0 + sa, rv);               // line k+NS-1 into line k-1's slot
             BRB_STAMP(t3);
             if (!has) {                                 // no line for this lane: nothing to write
                 e.any = false;
@@ -320,11 +328,14 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
         md5_seg_kernel<<<unsigned((n_rec + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, soff, slen, first, n_rec, out);
         return hipGetLastError();
     }
-    constexpr int W = 4;                               // 4 x 38 KiB of LDS: one workgroup per CU
+    constexpr int W = 4;                               // 4 x (8 NS + 14) KiB of LDS: one workgroup per CU
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-    md5_seg_line_kernel<W><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);
+    if (brb_opt::get(brb_opt::kLineSlots) == 2)
+        md5_seg_line_kernel<W, 2><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);
+    else
+        md5_seg_line_kernel<W, 3><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);
     return hipGetLastError();
 }
 

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
 // k+1 is in flight during line k-1's work.  An item's words go to the lane's 32-word funnel ring in
 // two halves per line, whole blocks compressed after each.  The return codes and the unsigned
 // long arithmetic of cur_offset / cur_remaining / cur_needed are unpack_lane's (the reference's).
-template <int W>
+template <int W, int NS>
 __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__restrict__ data,
                                                                 const uint64_t *__restrict__ offs,
                                                                 const uint32_t *__restrict__ lens, uint64_t n,
@@ -193,12 +193,13 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
     using namespace brb_line;
     constexpr uint32_t RW = brb_line::kRingWords;
     enum : uint32_t { kFields = 0, kData = 1, kCanary = 2, kDone = 3 };
-    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * kSlots * kSlot];
+    static_assert(NS == 2 || NS == 3, "two or three ring slots");
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[W * NS * kSlot];
     __shared__ __attribute__((aligned(8192))) uint32_t fring[W][RW][64];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n + 63) / 64;
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * kSlots * kSlot;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * NS * kSlot;
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
     Win win;
     win.init(lane);
@@ -227,7 +228,8 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         auto line_rel = [&](uint32_t j) { return j < nl ? rel0 + 128 * j : kOOB; };
         issue_rows(rs, lds0, line_rel(0), lane);
         issue_rows(rs, lds0 + kSlot, line_rel(1), lane);
-        issue_rows(rs, lds0 + 2 * kSlot, line_rel(2), lane);
+        if (NS == 3)
+            issue_rows(rs, lds0 + 2 * kSlot, line_rel(2), lane);
 
         int32_t code = BRB_METADATA_UNPACK_SUCCESS, item_count = 0, item = 0;
         uint32_t items = 0, phase = kDone, b = 0, dig[4] = {0, 0, 0, 0};
@@ -315,8 +317,8 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         };
         uint32_t sa = 0;                                         // byte offset of line k-1's slot (uniform)
         for (uint32_t k = 1; k <= K; k++) {
-            const uint32_t sb = sa == 2 * kSlot ? 0u : sa + kSlot;  // line k's slot
-            brb_dma::wait_vmcnt<8>();                            // line k landed; line k+1 may fly
+            const uint32_t sb = sa == (NS - 1) * kSlot ? 0u : sa + kSlot;  // line k's slot
+            brb_dma::wait_vmcnt<NS == 3 ? 8 : 0>();              // line k landed (NS = 3: line k+1 may fly)
             uint32_t dw[36];
             read_window(win, lds0 + sa, lds0 + sb, dw);
             // pack byte p sits at window byte p - L0 while L0 <= p < L0 + 256
@@ -360,8 +362,8 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
             } else {
                 events(L0, L0 + 128, lds0 + sa, lds0 + sb, dw, false);
             }
-            // line k+2 into line k-1's slot (its window reads are done)
-            issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + 2), lane);
+            // line k+NS-1 into line k-1's slot (its window reads are done)
+            issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + NS - 1), lane);
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
@@ -403,7 +405,10 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
     const uint64_t groups = (n + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-    metadata_line_kernel<W><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+    if (brb_opt::get(brb_opt::kLineSlots) == 2)
+        metadata_line_kernel<W, 2><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+    else
+        metadata_line_kernel<W, 3><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
     return hipGetLastError();
 }
 

@@ -20,10 +20,11 @@ enum Opt {
     kHostDigestChunkMiB = 7,   // 0: host-mode digest chunks of 32 MiB; k: k MiB
     kSegLine = 8,       // 1: segment digests / MetaData unpack on the line-staged kernels; 0: per-lane
     kB64Kernel = 9,     // 1: 64-byte fixed-stride records on digest_b64_kernel; 0: the generic DMA kernel
-    kCount = 10
+    kLineSlots = 10,    // LDS-DMA ring slots of the line-staged segment / MetaData kernels: 3 (default) or 2
+    kCount = 11
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1, 1, 3};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 
