@@ -1013,8 +1013,8 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"host_chunk_mib", brb_opt::kHostChunkMiB, 0, 1024},
                  {"host_digest_chunk_mib", brb_opt::kHostDigestChunkMiB, 0, 1024},
                  {"seg_line", brb_opt::kSegLine, 0, 1},
-                 {"b64_kernel", brb_opt::kB64Kernel, 0, 1},
-                 {"line_slots", brb_opt::kLineSlots, 2, 3}};
+                 {"b64_kernel", brb_opt::kB64Kernel, 0, 3},
+                 {"line_slots", brb_opt::kLineSlots, 0, 3}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -245,6 +245,64 @@ __global__ __launch_bounds__(64 * WAVES) void digest_b64_kernel(const uint8_t *_
     }
 }
 
+// Same work with one LDS slot per wave: a group's 16 words go to registers, and the next group's
+// DMA is issued into the same slot before the compression starts, so the registers are the second
+// buffer.  4 KiB of LDS per wave (50 VGPRs) lets 8 waves share a SIMD instead of 4.  A group's
+// digest is stored one iteration later, after that iteration's window read: the only VMEM
+// operation older than the DMA a wave waits for is then a store issued a whole compression
+// earlier, so the wait (vmcnt 0) never waits on a fresh write's acknowledgement.
+template <class Alg, int WAVES, bool OUT_ALIGNED>
+__global__ __launch_bounds__(64 * WAVES) void digest_b64r_kernel(const uint8_t *__restrict__ data, uint64_t n_rec,
+                                                                 uint8_t *__restrict__ out)
+{
+    using SG = brb_dma::Stager<1, false>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * SG::SLOT];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    uint64_t g = uint64_t(blockIdx.x) * WAVES + wv;
+    const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
+    if (g >= n_groups)
+        return;
+    uint8_t *my = ring + wv * SG::SLOT;
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(my));
+    const uint64_t last_full = n_rec / 64;
+    SG sg;
+    sg.init(64, uint32_t(g < last_full ? 64 : n_rec - g * 64), lane, true);
+    const uint64_t gbytes = wstride * 4096;
+    const uint8_t *base = data + g * 4096;
+    uint64_t left = (n_rec - g * 64) * 64;
+    sg.issue_fast(brb_dma::make_rsrc(base, left), lds0);
+    typename Alg::State prev;
+    uint64_t rprev = ~uint64_t(0);                            // no digest pending
+    for (;;) {
+        brb_dma::wait_vmcnt<0>();
+        uint32_t w[16];
+        sg.read(my, 0, w);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // the slot is free for the next DMA
+        if (rprev < n_rec)
+            Alg::template store<OUT_ALIGNED>(out, rprev, prev);
+        const uint64_t gn = g + wstride;
+        const bool more = gn < n_groups;
+        if (more) {
+            base += gbytes;
+            left -= gbytes;
+            if (gn >= last_full)
+                sg.group_offsets(64, uint32_t(n_rec - gn * 64), true);
+            sg.issue_fast(brb_dma::make_rsrc(base, left), lds0);
+        }
+        prev = Alg::iv();
+        Alg::compress(prev, w);
+        Alg::pad_only(prev, 64);
+        rprev = g * 64 + lane;
+        if (!more)
+            break;
+        g = gn;
+    }
+    if (rprev < n_rec)
+        Alg::template store<OUT_ALIGNED>(out, rprev, prev);
+}
+
 // Host-side launch.
 inline bool dma_supported(uint32_t rec_len)
 {
@@ -285,8 +343,17 @@ hipError_t launch_fixed_dma(const uint8_t *data, uint32_t rec_len, uint64_t n_re
             digest_fixed_dma_kernel<Alg, 8, 2, 2, true, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
         else
             digest_fixed_dma_kernel<Alg, 8, 2, 2, false, false, true><<<g, 512, 0, s>>>(data, rec_len, n_rec, out);
+    } else if (rec_len == 64 && brb_opt::get(brb_opt::kB64Kernel) >= 2) {
+        // register-buffered 64-byte kernel: 16 KiB per workgroup; option 2: 8 workgroups per CU
+        // (8 waves per SIMD), option 3: 4 per CU
+        const unsigned cap = brb_opt::get(brb_opt::kB64Kernel) == 2 ? 2048u : 1024u;
+        const unsigned g = unsigned(wgs_needed < cap ? wgs_needed : cap);
+        if (out_al)
+            digest_b64r_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, n_rec, out);
+        else
+            digest_b64r_kernel<Alg, W, false><<<g, 64 * W, 0, s>>>(data, n_rec, out);
     } else if (rec_len == 64 && brb_opt::get(brb_opt::kB64Kernel) != 0) {
-        // the lean 64-byte kernel, same shape as below (4 workgroups of 4 waves per CU, 16 KiB each)
+        // the lean 64-byte kernel, same shape as below (4 workgroups of 4 waves per CU, 32 KiB each)
         const unsigned g = unsigned(wgs_needed < 1024 ? wgs_needed : 1024);
         if (out_al)
             digest_b64_kernel<Alg, W, true><<<g, 64 * W, 0, s>>>(data, n_rec, out);

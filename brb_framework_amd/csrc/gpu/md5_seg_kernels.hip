@@ -332,7 +332,9 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
     const uint64_t groups = (n_rec + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-    if (brb_opt::get(brb_opt::kLineSlots) == 2)
+    // two slots by default: 40.6 vs 41.2 us with three (bench --op md5seg, interleaved A/B,
+    // gpurun_out/r04s_seg); test option line_slots 3 for the other
+    if (brb_opt::get(brb_opt::kLineSlots) != 3)
         md5_seg_line_kernel<W, 2><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);
     else
         md5_seg_line_kernel<W, 3><<<grid, 64 * W, 0, s>>>(data, soff, slen, first, n_rec, out);

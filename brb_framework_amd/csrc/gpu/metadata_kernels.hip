@@ -405,6 +405,8 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
     const uint64_t groups = (n + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
+    // three slots by default: 43.6 vs 49.3 us with two (bench --op metadata, interleaved A/B,
+    // gpurun_out/r04s_md); test option line_slots 2 for the other
     if (brb_opt::get(brb_opt::kLineSlots) == 2)
         metadata_line_kernel<W, 2><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
     else

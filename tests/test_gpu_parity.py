@@ -140,6 +140,23 @@ def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3])
+@pytest.mark.parametrize("n,off", [(1, 0), (64, 4), (65, 8), (4096 * 64 + 7, 0), (1 << 20, 12), (2048 * 4 * 64 * 3 + 65, 4)])
+def test_b64_kernels_exact_buffer(brb, orc, torch_dev, kernel, n, off):
+    """64-byte records (cfg3's shape) on each kernel the test option b64_kernel selects: 0 the
+    generic DMA kernel, 1 the lean two-slot kernel, 2 / 3 the register-buffered one-slot kernel at 8
+    / 4 waves per SIMD; partial last groups, several groups per wave, a buffer that ends at the batch."""
+    data = workload.gen_records(0x5EED0010, 0, n, 64)
+    d = torch_dev.zeros(off + data.size, dtype=torch_dev.uint8, device="cuda")
+    d[off:] = to_dev(torch_dev, data)
+    view = d[off:]
+    with brb.TestOption("b64_kernel", kernel):
+        got5 = brb.md5_batch_fixed(view, 64, n).cpu().numpy()
+        got1 = brb.sha1_batch_fixed(view, 64, n).cpu().numpy()
+    assert np.array_equal(got5, orc.md5_batch_fixed(data, 64, n, threads=16))
+    assert np.array_equal(got1, orc.sha1_batch_fixed(data, 64, n, threads=16))
+
+
 @pytest.mark.parametrize("n,rec_len,off", [
     (1, 4, 0), (63, 8, 4), (64, 64, 8), (65, 60, 12), (1000, 56, 0), (1001, 52, 4),
     (4097, 12, 0), (300_001, 32, 4), (270_000, 64, 0), (5000, 16, 8), (5000, 20, 0), (5000, 44, 12),

@@ -157,14 +157,15 @@ def infos_as_tuples(info):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seg_line", [1, 0])
-def test_unpack_batch_vs_oracle(brb, orc, seg_line):
-    """seg_line 1: the line-staged kernel (round 4), 0: the per-lane kernel."""
+@pytest.mark.parametrize("seg_line,slots", [(1, 3), (1, 2), (0, 0)])
+def test_unpack_batch_vs_oracle(brb, orc, seg_line, slots):
+    """seg_line 1: the line-staged kernel (round 4) with `slots` LDS-DMA ring slots (test option
+    line_slots), 0: the per-lane kernel."""
     packs = corpus(3, 4000)
     rng = np.random.default_rng(4)
     buf, offs, lens = scatter(rng, packs)
     want = [orc.metadata_unpack(p) for p in packs]
-    with brb.TestOption("seg_line", seg_line):
+    with brb.TestOption("seg_line", seg_line), brb.TestOption("line_slots", slots):
         got = infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens))      # host mode
         assert got == want
         import torch

@@ -41,15 +41,16 @@ def _want(orc, pool, offs, lens, first):
     return np.frombuffer(b"".join(out), np.uint8).reshape(-1, 16)
 
 
-@pytest.mark.parametrize("seg_line", [1, 0])
+@pytest.mark.parametrize("seg_line,slots", [(1, 2), (1, 3), (0, 0)])
 @pytest.mark.parametrize("seed,n_rec,max_segs,max_len", [(1, 300, 5, 40), (2, 200, 20, 7), (3, 64, 3, 3000),
                                                         (4, 1000, 1, 200), (5, 5, 200, 100), (6, 700, 40, 3),
                                                         (7, 257, 8, 130)])
-def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len, seg_line):
-    """seg_line 1: the line-staged kernel (line_stream.h; round 4), 0: the per-lane block kernel."""
+def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len, seg_line, slots):
+    """seg_line 1: the line-staged kernel (line_stream.h; round 4) with a ring of `slots` LDS-DMA
+    slots (test option line_slots), 0: the per-lane block kernel."""
     pool, offs, lens, first = _case(seed, n_rec, max_segs, max_len)
     want = _want(orc, pool, offs, lens, first)
-    with brb.TestOption("seg_line", seg_line):
+    with brb.TestOption("seg_line", seg_line), brb.TestOption("line_slots", slots):
         got = brb.md5_batch_segments(pool, offs, lens, first)
         assert np.array_equal(got, want)
         t = torch_dev
