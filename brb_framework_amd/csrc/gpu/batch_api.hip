@@ -1012,7 +1012,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"b64_group", brb_opt::kB64Group, -1, 6},
                  {"host_chunk_mib", brb_opt::kHostChunkMiB, 0, 1024},
                  {"host_digest_chunk_mib", brb_opt::kHostDigestChunkMiB, 0, 1024},
-                 {"seg_line", brb_opt::kSegLine, 0, 1},
+                 {"seg_line", brb_opt::kSegLine, 0, 2},
                  {"b64_kernel", brb_opt::kB64Kernel, 0, 3},
                  {"line_slots", brb_opt::kLineSlots, 0, 3}};
     if (!name) {

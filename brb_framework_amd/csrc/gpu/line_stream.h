@@ -105,8 +105,9 @@ BRB_DEV RowsV prep_rows(uint32_t rel, uint32_t lane)
     return r;
 }
 
-BRB_DEV void fire_rows(const brb_dma::v4i &rs, uint32_t lm, const RowsV &r)
+BRB_DEV void fire_rows(const brb_dma::v4i &rs, uint32_t lm_, const RowsV &r)
 {
+    const uint32_t lm = __builtin_amdgcn_readfirstlane(lm_);   // wave-uniform; says so to the compiler
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\t"
                  "s_mov_b32 m0, %10\n\t"
@@ -275,6 +276,28 @@ BRB_DEV void emit_finish(brb_md5::FunnelT<RW> &f, const Emit &p)
         f.nacc = p.rem;
         f.acc = p.rem ? (p.tail & ((1u << (8 * p.rem)) - 1u)) : 0u;
     }
+}
+
+// ---- producer / consumer wave pairs (md5_seg_pc_kernel, metadata_pc_kernel) ------------------
+// A pair's two waves share a funnel ring: the producer stages lines and emits message words, the
+// consumer compresses them.  Each publishes a running event count in LDS (one writer per counter,
+// release store after its ring / table writes; the reader's acquire load orders its reads after).
+// Every wait is bounded (~2^22 sleeps, far beyond any launch): a protocol fault ends the launch
+// with wrong digests, never a hung wave.
+BRB_DEV bool pc_wait_ge(uint32_t *ctr, uint32_t target)
+{
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(v) >= target)
+            return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
+{
+    __hip_atomic_store(ctr, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Compresses every whole block waiting in the ring (one compress site per call; at most two blocks

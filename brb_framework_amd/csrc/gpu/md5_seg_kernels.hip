@@ -315,6 +315,270 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
     }
 }
 
+// Producer / consumer form of the line-staged kernel.  With one 64-record group per SIMD (the
+// md5seg bench shape: 1 024 groups on 1 024 SIMDs) the lone wave of md5_seg_line_kernel pays the
+// lone-wave issue rate and every LDS round trip of its staging, emission and window reads (in-kernel
+// stamps, tools/seg_probe.py: 47 % compression, 53 % the rest).  Here a group belongs to a PAIR of
+// waves: the producer (waves 0..NP-1) walks the group's lines as md5_seg_line_kernel does (segment
+// table, DMA ring of two slots, window, emission) but never compresses; the consumer (wave NP + p)
+// compresses the words from the pair's 64-word funnel ring.  Both waves share a SIMD (8 waves per
+// CU), so the consumer's compression fills the producer's LDS and DMA waits and the two instruction
+// streams pair in the SIMD's issue.  Protocol (LDS event counts, pc_wait_ge / pc_publish):
+//   producer, per group: wait until the consumer is done with the previous group (ring and final
+//     state free); publish the plan (K lines, or 0: the group takes the per-lane path, run by the
+//     producer alone); per half-line hh (2K of them): wait until the consumer has taken halves
+//     0 .. hh-2 (so at most 15 + 17 + 17 words are in the 64-word ring), emit, publish wpos;
+//     then publish the carried bytes and the length;
+//   consumer, per group: read the plan; per half: read wpos, compress every whole block, publish;
+//     read the final state, pad, store the digest, publish.
+template <int NP>
+__global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__restrict__ data,
+                                                             const uint64_t *__restrict__ soff,
+                                                             const uint32_t *__restrict__ slen,
+                                                             const uint64_t *__restrict__ first, uint64_t n_rec,
+                                                             uint8_t *__restrict__ out)
+{
+    using namespace brb_line;
+    constexpr uint32_t RW = 64;                         // funnel ring words per lane (16 KiB per pair)
+    constexpr uint32_t kTab = 512;
+    __shared__ __attribute__((aligned(16384))) uint8_t ring[NP * 2 * kSlot];
+    __shared__ __attribute__((aligned(16384))) uint32_t fring[NP][RW][64];
+    __shared__ uint64_t tab_off[NP][kTab];
+    __shared__ uint32_t tab_len[NP][kTab];
+    __shared__ uint32_t wpx[NP][4][64];                 // wpos after half hh, slot hh % 4
+    __shared__ uint32_t fin[NP][3][64];                 // carried bytes | count << 24, length lo / hi
+    __shared__ uint32_t ev[NP][4];                      // producer events, consumer events, plan
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t pr = wv % NP;
+    const bool producer = wv < NP;
+    if (threadIdx.x < NP * 4)
+        (&ev[0][0])[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t n_groups = (n_rec + 63) / 64;
+    const uint64_t gstride = uint64_t(gridDim.x) * NP;
+
+    if (!producer) {
+        // ---------------- consumer ----------------
+        uint32_t pseen = 0, cev = 0;
+#ifdef BRB_LINE_STAMPS    // diagnostic builds only (tools/seg_probe.py): cycles the consumer waits for the producer
+        uint64_t c_wait = 0, c_t0 = __builtin_amdgcn_s_memtime();
+#define BRB_CWAIT(x) ({ const uint64_t _a = __builtin_amdgcn_s_memtime(); const bool _r = (x); c_wait += __builtin_amdgcn_s_memtime() - _a; _r; })
+#else
+#define BRB_CWAIT(x) (x)
+#endif
+        for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+                return;
+            pseen++;
+            const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
+            if (K == 0)
+                continue;                               // the producer ran this group alone
+            brb_md5::FunnelT<RW> f;
+            f.init(&fring[pr][0][lane]);
+            for (uint32_t hh = 0; hh < 2 * K; hh++) {
+                if (!BRB_CWAIT(pc_wait_ge(&ev[pr][0], pseen + 1)))
+                    return;
+                pseen++;
+                f.wpos = wpx[pr][hh & 3][lane];
+                pump_all(f);
+                pc_publish(&ev[pr][1], ++cev);
+            }
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+                return;
+            pseen++;
+            const uint32_t a = fin[pr][0][lane];
+            f.acc = a & 0xFFFFFFu;
+            f.nacc = a >> 24;
+            f.total = uint64_t(fin[pr][1][lane]) | (uint64_t(fin[pr][2][lane]) << 32);
+            const Md5State st = f.finish();
+            pc_publish(&ev[pr][1], ++cev);
+            const uint64_t rec = g * 64 + lane;
+#ifdef BRB_LINE_STAMPS
+            if (lane == 1 && rec < n_rec) {
+                const uint4 v = make_uint4(uint32_t(c_wait), uint32_t(__builtin_amdgcn_s_memtime() - c_t0), K, 0u);
+                __builtin_memcpy(out + 16 * rec, &v, 16);
+            }
+            if (lane == 1 || lane == 0)
+                continue;
+#endif
+            if (rec < n_rec)
+                store_digest(out, rec, st);
+        }
+        return;
+    }
+
+    // ---------------- producer ----------------
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + pr * 2 * kSlot;
+    const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    Win win;
+    win.init(lane);
+    uint32_t pev = 0, cbase = 0;                        // events published; consumer events expected so far
+#ifdef BRB_LINE_STAMPS    // the producer's waits for the consumer and for its DMA
+    uint64_t p_wait = 0, p_dma = 0;
+    const uint64_t p_t0 = __builtin_amdgcn_s_memtime();
+#define BRB_PWAIT(x) ({ const uint64_t _a = __builtin_amdgcn_s_memtime(); const bool _r = (x); p_wait += __builtin_amdgcn_s_memtime() - _a; _r; })
+#else
+#define BRB_PWAIT(x) (x)
+#endif
+    for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
+        if (!pc_wait_ge(&ev[pr][1], cbase))             // the consumer is done with the previous group
+            return;
+        const uint64_t rec = g * 64 + lane;
+        const bool valid = rec < n_rec;
+        const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
+        brb_md5::FunnelT<RW> f;
+        f.init(&fring[pr][0][lane]);
+        auto alone = [&]() {                            // the per-lane path, this wave only
+            ev[pr][2] = 0;
+            pc_publish(&ev[pr][0], ++pev);
+            if (valid) {
+                seg_lane(f, data, soff, slen, k0, k1);
+                store_digest(out, rec, f.finish());
+            }
+        };
+        const uint64_t s0 = brb_digest::uniform64(brb_digest::wave_min64(valid ? k0 : ~uint64_t(0)));
+        const uint64_t s1 = brb_digest::uniform64(brb_digest::wave_max64(valid ? k1 : 0));
+        const uint64_t S = s1 > s0 ? s1 - s0 : 0;
+        if (S > kTab) {
+            alone();
+            continue;
+        }
+        for (uint32_t i = lane; i < uint32_t(S); i += 64) {
+            tab_off[pr][i] = soff[s0 + i];
+            tab_len[pr][i] = slen[s0 + i];
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t t0 = uint32_t(k0 - (valid ? s0 : k0)), t1 = uint32_t(k1 - (valid ? s0 : k1));
+        uint64_t lo = ~uint64_t(0), hi = 0;
+        uint32_t nl = 0;
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t len = tab_len[pr][t];
+            if (!len) {
+                nl++;
+                continue;
+            }
+            const uint64_t a = dbase + tab_off[pr][t];
+            const uint64_t l0 = a & ~uint64_t(127), l1 = (a + len + 127) & ~uint64_t(127);
+            lo = l0 < lo ? l0 : lo;
+            hi = l1 > hi ? l1 : hi;
+            nl += uint32_t((l1 - l0) >> 7);
+        }
+        lo = brb_digest::uniform64(brb_digest::wave_min64(lo));
+        hi = brb_digest::uniform64(brb_digest::wave_max64(hi));
+        const uint32_t K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
+        if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {
+            alone();
+            continue;
+        }
+        ev[pr][2] = K;                                  // the plan (K >= 1)
+        pc_publish(&ev[pr][0], ++pev);
+        const brb_dma::v4i rs = group_rsrc(lo, hi);
+
+        constexpr uint32_t kEnd = 0xFFFFFFFFu;
+        uint32_t c_line = kEnd, c_last = 0, c_ss = 0, c_se = 0, nt = t0;
+        auto stage_line = [&]() -> LineDesc {
+            if (c_line == kEnd && nt < t1) {
+                const uint32_t len = tab_len[pr][nt];
+                if (len) {
+                    c_ss = uint32_t(dbase + tab_off[pr][nt] - lo);
+                    c_se = c_ss + len;
+                    c_line = c_ss & ~127u;
+                    c_last = (c_se - 1) & ~127u;
+                }
+                nt++;
+            }
+            const LineDesc d{c_line == kEnd ? kOOB : c_line, c_ss, c_se};
+            if (c_line != kEnd)
+                c_line = c_line == c_last ? kEnd : c_line + 128;
+            return d;
+        };
+        LineDesc dA = stage_line(), dB = stage_line();
+        issue_rows(rs, lds0, dA.line, lane);
+        issue_rows(rs, lds0 + kSlot, dB.line, lane);
+        uint32_t b = 0, sa = 0;
+        bool ok = true;
+        for (uint32_t k = 1; k <= K && ok; k++) {
+            const uint32_t sb = sa ^ kSlot;             // line k's slot
+            const LineDesc dn = stage_line();           // line k+1
+            const RowsV rv = prep_rows(dn.line, lane);
+#ifdef BRB_LINE_STAMPS
+            const uint64_t _d0 = __builtin_amdgcn_s_memtime();
+            brb_dma::wait_vmcnt<0>();
+            p_dma += __builtin_amdgcn_s_memtime() - _d0;
+#else
+            brb_dma::wait_vmcnt<0>();                   // line k landed
+#endif
+            uint32_t dw[36];
+            read_window(win, lds0 + sa, lds0 + sb, dw);
+            const LineDesc d = dA;
+            dA = dB;
+            dB = dn;
+            const bool has = d.line != kOOB;
+            const bool whole = has && d.ss < d.line && d.se - d.line > 128u + b;
+            const bool all_whole = __builtin_amdgcn_ballot_w64(has && !whole) == 0;
+            Emit e;
+            if (all_whole) {
+                plan_whole(f, b, e);
+            } else {
+                const bool fst = d.ss >= d.line;
+                if (has && fst)
+                    f.total += d.se - d.ss;
+                plan_range(f, fst, d.ss - d.line, d.se - d.line < 4096u ? d.se - d.line : 4096u, b, e);
+                if (has)
+                    edge_words(win, lds0 + sa, lds0 + sb, e);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+            }
+            fire_rows(rs, lds0 + sa, rv);               // line k+1 into line k-1's slot
+            const uint32_t hh = 2 * (k - 1);
+            // half 0: the consumer has taken halves 0 .. hh-2 of this group
+            if (hh >= 2 && !BRB_PWAIT(pc_wait_ge(&ev[pr][1], cbase + hh - 1))) {
+                ok = false;
+                break;
+            }
+            if (has) {
+                if (all_whole)
+                    emit_half<RW, 0, true>(f, e, dw);
+                else
+                    emit_half<RW, 0, false>(f, e, dw);
+            }
+            wpx[pr][hh & 3][lane] = f.wpos;
+            pc_publish(&ev[pr][0], ++pev);
+            if (!BRB_PWAIT(pc_wait_ge(&ev[pr][1], cbase + hh))) {   // half hh + 1: halves 0 .. hh-1 taken
+                ok = false;
+                break;
+            }
+            if (has) {
+                if (all_whole)
+                    emit_half<RW, 1, true>(f, e, dw);
+                else
+                    emit_half<RW, 1, false>(f, e, dw);
+                emit_finish(f, e);
+            }
+            wpx[pr][(hh + 1) & 3][lane] = f.wpos;
+            pc_publish(&ev[pr][0], ++pev);
+            sa = sb;
+        }
+        brb_dma::wait_vmcnt<0>();                       // the stray stage past K, before the slots are reused
+        if (!ok)
+            return;
+        fin[pr][0][lane] = uint32_t(f.acc) | (f.nacc << 24);
+        fin[pr][1][lane] = uint32_t(f.total);
+        fin[pr][2][lane] = uint32_t(f.total >> 32);
+        pc_publish(&ev[pr][0], ++pev);
+        cbase += 2 * K + 1;
+#ifdef BRB_LINE_STAMPS
+        if (lane == 0 && valid) {
+            const uint4 v = make_uint4(uint32_t(p_wait), uint32_t(p_dma), uint32_t(__builtin_amdgcn_s_memtime() - p_t0), K);
+            __builtin_memcpy(out + 16 * rec, &v, 16);
+        }
+#endif
+    }
+#undef BRB_PWAIT
+#undef BRB_CWAIT
+}
+
 }  // namespace
 
 namespace brb {
@@ -328,8 +592,15 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
         md5_seg_kernel<<<unsigned((n_rec + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, soff, slen, first, n_rec, out);
         return hipGetLastError();
     }
-    constexpr int W = 4;                               // 4 x (8 NS + 14) KiB of LDS: one workgroup per CU
     const uint64_t groups = (n_rec + 63) / 64;
+    if (brb_opt::get(brb_opt::kSegLine) == 2) {
+        constexpr int NP = 4;                          // 4 pairs, 159 KiB of LDS: one workgroup per CU
+        const uint64_t wgs = (groups + NP - 1) / NP;
+        const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
+        md5_seg_pc_kernel<NP><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out);
+        return hipGetLastError();
+    }
+    constexpr int W = 4;                               // 4 x (8 NS + 14) KiB of LDS: one workgroup per CU
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
     // two slots by default: 40.6 vs 41.2 us with three (bench --op md5seg, interleaved A/B,

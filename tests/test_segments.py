@@ -41,13 +41,14 @@ def _want(orc, pool, offs, lens, first):
     return np.frombuffer(b"".join(out), np.uint8).reshape(-1, 16)
 
 
-@pytest.mark.parametrize("seg_line,slots", [(1, 2), (1, 3), (0, 0)])
+@pytest.mark.parametrize("seg_line,slots", [(1, 2), (1, 3), (2, 0), (0, 0)])
 @pytest.mark.parametrize("seed,n_rec,max_segs,max_len", [(1, 300, 5, 40), (2, 200, 20, 7), (3, 64, 3, 3000),
                                                         (4, 1000, 1, 200), (5, 5, 200, 100), (6, 700, 40, 3),
                                                         (7, 257, 8, 130)])
 def test_segments_vs_hashlib(brb, orc, torch_dev, seed, n_rec, max_segs, max_len, seg_line, slots):
     """seg_line 1: the line-staged kernel (line_stream.h; round 4) with a ring of `slots` LDS-DMA
-    slots (test option line_slots), 0: the per-lane block kernel."""
+    slots (test option line_slots), 2: its producer / consumer wave-pair form, 0: the per-lane block
+    kernel."""
     pool, offs, lens, first = _case(seed, n_rec, max_segs, max_len)
     want = _want(orc, pool, offs, lens, first)
     with brb.TestOption("seg_line", seg_line), brb.TestOption("line_slots", slots):
@@ -76,7 +77,8 @@ def _pack_items_case(n, K, Q, gap, seed):
 
 @pytest.mark.parametrize("n,K,Q,gap,seed", [(65536, 4, 375, 25, 0), (4097, 4, 375, 25, 1), (3000, 9, 61, 3, 2),
                                             (2000, 3, 700, 130, 3), (1024, 16, 4, 1, 4), (640, 2, 1, 0, 5)])
-def test_segments_pack_layout(brb, orc, torch_dev, n, K, Q, gap, seed):
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_pack_layout(brb, orc, torch_dev, n, K, Q, gap, seed, seg_line):
     """Segments as the MetaData items of back-to-back packs (the md5seg bench shape at full size
     and variants: ragged sizes, items sharing memory lines, 1..4-byte items), line-staged kernel vs
     the per-lane kernel vs hashlib on sampled records (every record for the smaller shapes)."""
@@ -84,7 +86,8 @@ def test_segments_pack_layout(brb, orc, torch_dev, n, K, Q, gap, seed):
     pool, offs, lens, first = _pack_items_case(n, K, Q, gap, seed)
     dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
     d, o, ln, fi = dev(pool), dev(offs), dev(lens), dev(first)
-    got = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
     with brb.TestOption("seg_line", 0):
         ref = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
     assert np.array_equal(got, ref)
@@ -95,7 +98,8 @@ def test_segments_pack_layout(brb, orc, torch_dev, n, K, Q, gap, seed):
         assert got[i].tobytes() == hashlib.md5(msg).digest(), i
 
 
-def test_segments_mixed_wide_groups(brb, torch_dev):
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_mixed_wide_groups(brb, torch_dev, seg_line):
     """One launch with groups whose segments lie within 2 GiB (line-staged) and groups whose
     segments lie more than 2 GiB apart (32-bit DMA offsets cannot reach: the per-lane path), 640
     records in 10 groups, every other group wide."""
@@ -121,7 +125,8 @@ def test_segments_mixed_wide_groups(brb, torch_dev):
         wide[int(first[r])] = True
     offs[wide] += far
     dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
-    got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
     for i in range(n):
         parts = []
         for k in range(int(first[i]), int(first[i + 1])):
@@ -159,7 +164,8 @@ def test_segments_empty_and_sub_ranges(brb):
     assert got[2].tobytes() == hashlib.md5(pool[10:43].tobytes()).digest()
 
 
-def test_segments_at_buffer_ends(brb, orc, torch_dev):
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_at_buffer_ends(brb, orc, torch_dev, seg_line):
     """Segments that start at the device buffer's first byte (a range that would begin up to 3
     bytes before it) and end at its last byte, in a buffer of exactly the pool's size; 130 records
     (a partial last wave), lengths 1..200."""
@@ -178,12 +184,14 @@ def test_segments_at_buffer_ends(brb, orc, torch_dev):
     offs[sel] = pool.size - lens[sel]
     want = _want(orc, pool, offs, lens, first)
     t = torch_dev
-    dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
-                                 t.from_numpy(first).cuda())
+    with brb.TestOption("seg_line", seg_line):
+        dev = brb.md5_batch_segments(t.from_numpy(pool).cuda(), t.from_numpy(offs).cuda(), t.from_numpy(lens).cuda(),
+                                     t.from_numpy(first).cuda())
     assert np.array_equal(dev.cpu().numpy(), want)
 
 
-def test_segments_beyond_4gib(brb, torch_dev):
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_beyond_4gib(brb, torch_dev, seg_line):
     """Segment offsets past 2^32 in one 4.5 GiB device buffer: 500 records of 1..6 segments
     (0..700 bytes), some straddling byte offsets 2^31 and 2^32, against hashlib on host copies of
     just those segments."""
@@ -206,7 +214,8 @@ def test_segments_beyond_4gib(brb, torch_dev):
         offs[i], lens[i] = o, 700
     segs = [d[int(o):int(o) + int(m)].cpu().numpy().tobytes() for o, m in zip(offs, lens)]
     dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
-    got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
     for i in range(n_rec):
         msg = b"".join(segs[k] for k in range(int(first[i]), int(first[i + 1])))
         assert got[i].tobytes() == hashlib.md5(msg).digest(), i

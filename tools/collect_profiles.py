@@ -116,8 +116,8 @@ def main():
                                ("pmc4", "cfg4_blowfish", "bf_rep_kernel", 1),
                                ("pmc_rc4", "f1_rc4", "rc4_crypt_kernel", 1),
                                ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2),
-                               ("pmc_md", "f4_metadata", "metadata_unpack", 1),
-                               ("pmc_seg", "f4_md5seg", "md5_seg_kernel", 1),
+                               ("pmc_md", "f4_metadata", "metadata_", 1),
+                               ("pmc_seg", "f4_md5seg", "md5_seg_", 1),
                                ("pmc_b64", "f4_base64", "b64_", 2),
                                ("pmc_md5var", "var_md5var", "Md5Alg", 1),
                                ("pmc_sha1var", "var_sha1var", "Sha1Alg", 1)):

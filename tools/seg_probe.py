@@ -2,7 +2,8 @@
 """Where a wave of the line-staged segment kernel spends its cycles (in-kernel s_memtime stamps).
 
 Run with the diagnostic library (make -C brb_framework_amd diag):
-    BRB_CRYPTO_LIB=brb_framework_amd/build-diag/libbrb_crypto_gpu.so python3 tools/seg_probe.py
+    BRB_CRYPTO_LIB=brb_framework_amd/build-diag/libbrb_crypto_gpu.so python3 tools/seg_probe.py [--pc]
+(--pc: the producer / consumer kernel, seg_line 2: each wave's waits for the other and the DMA)
 The diagnostic md5_seg_line_kernel writes, instead of digests, per group: into record 64g's slot the
 cycles spent in the top-of-line DMA wait, the window read, the stage (cursor + DMA issue) and the
 word emission; into record 64g+1's slot the pumps (compressions), the group's total and its line
@@ -32,11 +33,19 @@ def main():
     first = (np.arange(n + 1, dtype=np.uint64) * K).astype(np.uint64)
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
     d, o, ln, fi = dev(pool), dev(offs), dev(lens), dev(first)
-    for _ in range(20):
-        out = brb.md5_batch_segments(d, o, ln, fi)
+    pc = "--pc" in sys.argv
+    with brb.TestOption("seg_line", 2 if pc else 1):
+        for _ in range(20):
+            out = brb.md5_batch_segments(d, o, ln, fi)
     torch.cuda.synchronize()
     v = out.cpu().numpy().reshape(-1).view(np.uint32).reshape(n, 4)
     a, b = v[0::64], v[1::64]
+    if pc:      # producer: waits for the consumer, DMA waits, total, K; consumer: waits, total, K
+        pt, ct = a[:, 2].astype(np.float64), b[:, 1].astype(np.float64)
+        print(f"groups {len(pt)}, K {int(np.median(a[:, 3]))}; producer total {np.median(pt):.0f} cycles: "
+              f"waits for the consumer {np.median(a[:, 0] / pt):.3f}, for its DMA {np.median(a[:, 1] / pt):.3f}; "
+              f"consumer total {np.median(ct):.0f}: waits for the producer {np.median(b[:, 0] / ct):.3f}")
+        return
     parts = {"wait": a[:, 0], "window": a[:, 1], "stage": a[:, 2], "emit": a[:, 3], "pump": b[:, 0]}
     total = b[:, 1].astype(np.float64)
     print(f"groups {len(total)}, lines per group (median) {int(np.median(b[:, 2]))}, "
