@@ -300,6 +300,29 @@ BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
     __hip_atomic_store(ctr, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+BRB_DEV uint32_t pc_load(uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Producer side, per lane: wait until the lane's ring has room for a half-line of words (at most
+// 17, plus the free slot past them that emit_half's clamp may write): wpos - cpos <= RW - 18, cpos
+// being the consumer's published count of compressed words.  Lanes that will not write pass.
+template <uint32_t RW>
+BRB_DEV bool pc_room(uint32_t *cpx, uint32_t wpos, bool writes, uint64_t *idle = nullptr)
+{
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+        const bool full = writes && wpos - pc_load(cpx) > RW - 18;
+        if (__builtin_amdgcn_ballot_w64(full) == 0)
+            return true;
+        const uint64_t t = idle ? __builtin_amdgcn_s_memtime() : 0;
+        __builtin_amdgcn_s_sleep(1);
+        if (idle)
+            *idle += __builtin_amdgcn_s_memtime() - t;
+    }
+    return false;
+}
+
 // Compresses every whole block waiting in the ring (one compress site per call; at most two blocks
 // wait after a half).
 template <uint32_t RW>
@@ -307,6 +330,60 @@ BRB_DEV void pump_all(brb_md5::FunnelT<RW> &f)
 {
     while (f.wpos - f.cpos >= 16)
         f.pump();
+}
+
+// One line's emission in two halves (the range planned in e).  Alone (PC = false): whole blocks are
+// compressed after each half (a 32-word ring).  Producer (PC = true): before each half, room in the
+// pair's ring (pc_room); after it, the word count posted to the consumer (wpx).  `writes`: this lane
+// has words in the line.  False when a wait timed out.
+template <uint32_t RW, bool WHOLE, bool PC>
+BRB_DEV bool emit_line(brb_md5::FunnelT<RW> &f, Emit &e, const uint32_t (&dw)[36], bool writes, uint32_t *cpx,
+                       uint32_t *wpx, uint64_t *idle = nullptr)
+{
+    if (PC && !pc_room<RW>(cpx, f.wpos, writes, idle))
+        return false;
+    if (writes)
+        emit_half<RW, 0, WHOLE>(f, e, dw);
+    if (PC)
+        pc_publish(wpx, f.wpos);
+    else
+        pump_all(f);
+    if (PC && !pc_room<RW>(cpx, f.wpos, writes, idle))
+        return false;
+    if (writes) {
+        emit_half<RW, 1, WHOLE>(f, e, dw);
+        emit_finish(f, e);
+    }
+    if (PC)
+        pc_publish(wpx, f.wpos);
+    else
+        pump_all(f);
+    return true;
+}
+
+// Consumer: compresses the lane's words as the producer posts them (wpx), posting its own count
+// (cpx), until the producer's event count reaches `end` (its last post is in by then).  False when
+// the producer never got there (a protocol fault; the launch's digests are then wrong, but it ends).
+template <uint32_t RW>
+BRB_DEV bool pc_consume(brb_md5::FunnelT<RW> &f, uint32_t *ev_p, uint32_t end, uint32_t *wpx, uint32_t *cpx,
+                        uint64_t *idle = nullptr)
+{
+    for (uint32_t spin = 0; spin < (1u << 24); spin++) {
+        const bool ended = __builtin_amdgcn_readfirstlane(pc_load(ev_p)) >= end;   // before wpos: the last post is in
+        f.wpos = pc_load(wpx);
+        if (__builtin_amdgcn_ballot_w64(f.wpos - f.cpos >= 16) != 0) {
+            pump_all(f);
+            pc_publish(cpx, f.cpos);
+        } else if (ended) {
+            return true;
+        } else {
+            const uint64_t t = idle ? __builtin_amdgcn_s_memtime() : 0;
+            __builtin_amdgcn_s_sleep(1);
+            if (idle)
+                *idle += __builtin_amdgcn_s_memtime() - t;
+        }
+    }
+    return false;
 }
 
 }  // namespace brb_line

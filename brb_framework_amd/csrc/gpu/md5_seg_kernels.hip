@@ -323,14 +323,14 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
 // table, DMA ring of two slots, window, emission) but never compresses; the consumer (wave NP + p)
 // compresses the words from the pair's 64-word funnel ring.  Both waves share a SIMD (8 waves per
 // CU), so the consumer's compression fills the producer's LDS and DMA waits and the two instruction
-// streams pair in the SIMD's issue.  Protocol (LDS event counts, pc_wait_ge / pc_publish):
-//   producer, per group: wait until the consumer is done with the previous group (ring and final
-//     state free); publish the plan (K lines, or 0: the group takes the per-lane path, run by the
-//     producer alone); per half-line hh (2K of them): wait until the consumer has taken halves
-//     0 .. hh-2 (so at most 15 + 17 + 17 words are in the 64-word ring), emit, publish wpos;
-//     then publish the carried bytes and the length;
-//   consumer, per group: read the plan; per half: read wpos, compress every whole block, publish;
-//     read the final state, pad, store the digest, publish.
+// streams pair in the SIMD's issue.
+// Protocol, per lane, through LDS mailboxes (line_stream.h pc_*): the producer posts its word count
+// wpos after each half-line (release store) and waits, before a half, until the consumer's posted
+// compressed count cpos leaves room in the ring (pc_room); the consumer polls wpos, compresses every
+// whole block, posts cpos.  Per group, two event counts order the rest: the producer publishes the
+// group's plan (K lines, or 0: the per-lane path, run by the producer alone) and its end (the carried
+// bytes and the length in `fin`); the consumer acknowledges the plan and, after the digest, the end
+// (its cpos back to 0).  A producer starts a group only once every earlier event is acknowledged.
 template <int NP>
 __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ soff,
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     __shared__ __attribute__((aligned(16384))) uint32_t fring[NP][RW][64];
     __shared__ uint64_t tab_off[NP][kTab];
     __shared__ uint32_t tab_len[NP][kTab];
-    __shared__ uint32_t wpx[NP][4][64];                 // wpos after half hh, slot hh % 4
+    __shared__ uint32_t wpx[NP][64], cpx[NP][64];       // the mailboxes: words written, words compressed
     __shared__ uint32_t fin[NP][3][64];                 // carried bytes | count << 24, length lo / hi
     __shared__ uint32_t ev[NP][4];                      // producer events, consumer events, plan
     const uint32_t lane = threadIdx.x & 63;
@@ -354,6 +354,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     const bool producer = wv < NP;
     if (threadIdx.x < NP * 4)
         (&ev[0][0])[threadIdx.x] = 0;
+    if (threadIdx.x < NP * 64) {
+        (&wpx[0][0])[threadIdx.x] = 0;
+        (&cpx[0][0])[threadIdx.x] = 0;
+    }
     __syncthreads();
     const uint64_t n_groups = (n_rec + 63) / 64;
     const uint64_t gstride = uint64_t(gridDim.x) * NP;
@@ -361,45 +365,42 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     if (!producer) {
         // ---------------- consumer ----------------
         uint32_t pseen = 0, cev = 0;
-#ifdef BRB_LINE_STAMPS    // diagnostic builds only (tools/seg_probe.py): cycles the consumer waits for the producer
-        uint64_t c_wait = 0, c_t0 = __builtin_amdgcn_s_memtime();
-#define BRB_CWAIT(x) ({ const uint64_t _a = __builtin_amdgcn_s_memtime(); const bool _r = (x); c_wait += __builtin_amdgcn_s_memtime() - _a; _r; })
-#else
-#define BRB_CWAIT(x) (x)
+#ifdef BRB_LINE_STAMPS    // diagnostic builds only (tools/seg_probe.py --pc): cycles without a block to compress
+        uint64_t c_wait = 0;
+        const uint64_t c_t0 = __builtin_amdgcn_s_memtime();
 #endif
         for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
             if (!pc_wait_ge(&ev[pr][0], pseen + 1))
                 return;
             pseen++;
             const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
+            pc_publish(&ev[pr][1], ++cev);              // plan read
             if (K == 0)
-                continue;                               // the producer ran this group alone
+                continue;                               // the producer runs this group alone
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
-            for (uint32_t hh = 0; hh < 2 * K; hh++) {
-                if (!BRB_CWAIT(pc_wait_ge(&ev[pr][0], pseen + 1)))
-                    return;
-                pseen++;
-                f.wpos = wpx[pr][hh & 3][lane];
-                pump_all(f);
-                pc_publish(&ev[pr][1], ++cev);
-            }
-            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+#ifdef BRB_LINE_STAMPS
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &c_wait))
                 return;
+#else
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane]))
+                return;
+#endif
             pseen++;
             const uint32_t a = fin[pr][0][lane];
             f.acc = a & 0xFFFFFFu;
             f.nacc = a >> 24;
             f.total = uint64_t(fin[pr][1][lane]) | (uint64_t(fin[pr][2][lane]) << 32);
             const Md5State st = f.finish();
-            pc_publish(&ev[pr][1], ++cev);
+            pc_publish(&cpx[pr][lane], 0u);
+            pc_publish(&ev[pr][1], ++cev);              // group done: ring, fin and cpos free
             const uint64_t rec = g * 64 + lane;
 #ifdef BRB_LINE_STAMPS
             if (lane == 1 && rec < n_rec) {
                 const uint4 v = make_uint4(uint32_t(c_wait), uint32_t(__builtin_amdgcn_s_memtime() - c_t0), K, 0u);
                 __builtin_memcpy(out + 16 * rec, &v, 16);
             }
-            if (lane == 1 || lane == 0)
+            if (lane < 2)
                 continue;
 #endif
             if (rec < n_rec)
@@ -413,16 +414,13 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
     Win win;
     win.init(lane);
-    uint32_t pev = 0, cbase = 0;                        // events published; consumer events expected so far
-#ifdef BRB_LINE_STAMPS    // the producer's waits for the consumer and for its DMA
+    uint32_t pev = 0, cexp = 0;                         // events published; consumer events expected so far
+#ifdef BRB_LINE_STAMPS    // the producer's waits for ring room and for its DMA
     uint64_t p_wait = 0, p_dma = 0;
     const uint64_t p_t0 = __builtin_amdgcn_s_memtime();
-#define BRB_PWAIT(x) ({ const uint64_t _a = __builtin_amdgcn_s_memtime(); const bool _r = (x); p_wait += __builtin_amdgcn_s_memtime() - _a; _r; })
-#else
-#define BRB_PWAIT(x) (x)
 #endif
     for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
-        if (!pc_wait_ge(&ev[pr][1], cbase))             // the consumer is done with the previous group
+        if (!pc_wait_ge(&ev[pr][1], cexp))             // every earlier event acknowledged
             return;
         const uint64_t rec = g * 64 + lane;
         const bool valid = rec < n_rec;
@@ -432,6 +430,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         auto alone = [&]() {                            // the per-lane path, this wave only
             ev[pr][2] = 0;
             pc_publish(&ev[pr][0], ++pev);
+            cexp += 1;
             if (valid) {
                 seg_lane(f, data, soff, slen, k0, k1);
                 store_digest(out, rec, f.finish());
@@ -472,8 +471,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             alone();
             continue;
         }
+        wpx[pr][lane] = 0;                              // the consumer reads it only after the plan
         ev[pr][2] = K;                                  // the plan (K >= 1)
         pc_publish(&ev[pr][0], ++pev);
+        cexp += 2;
         const brb_dma::v4i rs = group_rsrc(lo, hi);
 
         constexpr uint32_t kEnd = 0xFFFFFFFFu;
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         issue_rows(rs, lds0 + kSlot, dB.line, lane);
         uint32_t b = 0, sa = 0;
         bool ok = true;
-        for (uint32_t k = 1; k <= K && ok; k++) {
+        for (uint32_t k = 1; k <= K; k++) {
             const uint32_t sb = sa ^ kSlot;             // line k's slot
             const LineDesc dn = stage_line();           // line k+1
             const RowsV rv = prep_rows(dn.line, lane);
@@ -531,33 +532,17 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
                 __builtin_amdgcn_s_waitcnt(0xC07F);
             }
             fire_rows(rs, lds0 + sa, rv);               // line k+1 into line k-1's slot
-            const uint32_t hh = 2 * (k - 1);
-            // half 0: the consumer has taken halves 0 .. hh-2 of this group
-            if (hh >= 2 && !BRB_PWAIT(pc_wait_ge(&ev[pr][1], cbase + hh - 1))) {
+#ifdef BRB_LINE_STAMPS
+            uint64_t *idle = &p_wait;
+#else
+            uint64_t *idle = nullptr;
+#endif
+            const bool emitted = all_whole ? emit_line<RW, true, true>(f, e, dw, has, &cpx[pr][lane], &wpx[pr][lane], idle)
+                                           : emit_line<RW, false, true>(f, e, dw, has, &cpx[pr][lane], &wpx[pr][lane], idle);
+            if (!emitted) {
                 ok = false;
                 break;
             }
-            if (has) {
-                if (all_whole)
-                    emit_half<RW, 0, true>(f, e, dw);
-                else
-                    emit_half<RW, 0, false>(f, e, dw);
-            }
-            wpx[pr][hh & 3][lane] = f.wpos;
-            pc_publish(&ev[pr][0], ++pev);
-            if (!BRB_PWAIT(pc_wait_ge(&ev[pr][1], cbase + hh))) {   // half hh + 1: halves 0 .. hh-1 taken
-                ok = false;
-                break;
-            }
-            if (has) {
-                if (all_whole)
-                    emit_half<RW, 1, true>(f, e, dw);
-                else
-                    emit_half<RW, 1, false>(f, e, dw);
-                emit_finish(f, e);
-            }
-            wpx[pr][(hh + 1) & 3][lane] = f.wpos;
-            pc_publish(&ev[pr][0], ++pev);
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                       // the stray stage past K, before the slots are reused
@@ -566,8 +551,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         fin[pr][0][lane] = uint32_t(f.acc) | (f.nacc << 24);
         fin[pr][1][lane] = uint32_t(f.total);
         fin[pr][2][lane] = uint32_t(f.total >> 32);
-        pc_publish(&ev[pr][0], ++pev);
-        cbase += 2 * K + 1;
+        pc_publish(&ev[pr][0], ++pev);                  // the group's end
 #ifdef BRB_LINE_STAMPS
         if (lane == 0 && valid) {
             const uint4 v = make_uint4(uint32_t(p_wait), uint32_t(p_dma), uint32_t(__builtin_amdgcn_s_memtime() - p_t0), K);
@@ -575,8 +559,6 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         }
 #endif
     }
-#undef BRB_PWAIT
-#undef BRB_CWAIT
 }
 
 }  // namespace
