@@ -173,38 +173,108 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
 }
 
 // Line-staged MetaDataUnpack (round 4; line_stream.h).  A wave unpacks groups of 64 packs, one per
-// lane; a pack's 128-byte lines stream through the two-slot LDS-DMA ring, and the lane walks its pack
-// out of the window (lines k-1, k) as a state machine over the reference's loop (meta_data.c:202-282):
+// lane; a pack's 128-byte lines stream through the LDS-DMA ring, and the lane walks its pack out of
+// the window (lines k-1, k) as a state machine over the reference's loop (meta_data.c:202-282):
 //   FIELDS at `offset`: the loop's checks, sz from the item's fields (window bytes), -> DATA
 //   DATA [ds, de):       the item's words that start in line k-1 emitted into the funnel ring;
 //                        -> CANARY once its last word is out
 //   CANARY at de:        the 0x1F check, items++, offset == size stops the walk, -> FIELDS
 // Every event is handled in the line that holds its first byte, so the window always holds what it
-// reads; the whole line's reads happen before that line's slot is refilled.  Three ring slots: line
-// k+1 is in flight during line k-1's work.  An item's words go to the lane's 32-word funnel ring in
-// two halves per line, whole blocks compressed after each.  The return codes and the unsigned
-// long arithmetic of cur_offset / cur_remaining / cur_needed are unpack_lane's (the reference's).
-template <int W, int NS>
-__global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__restrict__ data,
-                                                                const uint64_t *__restrict__ offs,
-                                                                const uint32_t *__restrict__ lens, uint64_t n,
-                                                                BRB_MetaDataUnpackInfo *__restrict__ info)
+// reads; the whole line's reads happen before that line's slot is refilled.  NS ring slots (three:
+// line k+1 is in flight during line k-1's work).  The return codes and the unsigned long arithmetic
+// of cur_offset / cur_remaining / cur_needed are unpack_lane's (the reference's).
+// PC = false: the walking wave also compresses (a 32-word funnel ring, whole blocks compressed after
+// each half-line).  PC = true: wave pairs as md5_seg_pc_kernel (md5_seg_kernels.hip): the walking
+// wave (the producer) emits the words into the pair's 64-word ring; its partner on the same SIMD
+// (wave W + p) compresses them, pads, checks the digest and writes the info (two ring slots, so that
+// four pairs fit a CU's LDS).
+template <int W, int NS, bool PC>
+__global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(const uint8_t *__restrict__ data,
+                                                                               const uint64_t *__restrict__ offs,
+                                                                               const uint32_t *__restrict__ lens, uint64_t n,
+                                                                               BRB_MetaDataUnpackInfo *__restrict__ info)
 {
     using namespace brb_line;
-    constexpr uint32_t RW = brb_line::kRingWords;
+    constexpr uint32_t RW = PC ? 64 : brb_line::kRingWords;
+    constexpr int WP = PC ? W : 1;                      // pairs' mailbox arrays (1: unused)
     enum : uint32_t { kFields = 0, kData = 1, kCanary = 2, kDone = 3 };
     static_assert(NS == 2 || NS == 3, "two or three ring slots");
+    static_assert(!PC || NS == 2, "wave pairs: two slots");
     __shared__ __attribute__((aligned(16384))) uint8_t ring[W * NS * kSlot];
-    __shared__ __attribute__((aligned(8192))) uint32_t fring[W][RW][64];
+    __shared__ __attribute__((aligned(RW * 256))) uint32_t fring[W][RW][64];
+    __shared__ uint32_t wpx[WP][64], cpx[WP][64];       // pairs: words written, words compressed
+    __shared__ uint32_t fin[WP][15][64];                // pairs: the walk's results for the consumer
+    __shared__ uint32_t ev[WP][4];                      // pairs: producer events, consumer events, plan
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t pr = PC ? wv % W : wv;
     const uint64_t n_groups = (n + 63) / 64;
-    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + wv * NS * kSlot;
+    const uint64_t gstride = uint64_t(gridDim.x) * W;
+    if (PC) {
+        if (threadIdx.x < WP * 4)
+            (&ev[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < WP * 64) {
+            (&wpx[0][0])[threadIdx.x] = 0;
+            (&cpx[0][0])[threadIdx.x] = 0;
+        }
+        __syncthreads();
+    }
+    if (PC && wv >= W) {
+        // ---------------- consumer ----------------
+        uint32_t pseen = 0, cev = 0;
+        for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+                return;
+            pseen++;
+            const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
+            pc_publish(&ev[pr][1], ++cev);              // plan read
+            if (K == 0)
+                continue;                               // the producer runs this group alone
+            brb_md5::FunnelT<RW> f;
+            f.init(&fring[pr][0][lane]);
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane]))
+                return;
+            pseen++;
+            uint32_t v[15];
+#pragma unroll
+            for (int q = 0; q < 15; q++)
+                v[q] = fin[pr][q][lane];
+            f.acc = v[0] & 0xFFFFFFu;
+            f.nacc = v[0] >> 24;
+            f.total = uint64_t(v[1]) | (uint64_t(v[2]) << 32);
+            int32_t code = int32_t(v[3]);
+            if (code == BRB_METADATA_UNPACK_SUCCESS) {  // :287-298
+                const Md5State st = f.finish();
+                if (st.a != v[4] || st.b != v[5] || st.c != v[6] || st.d != v[7])
+                    code = BRB_METADATA_UNPACK_FAILED_DIGEST_INVALID;
+            }
+            pc_publish(&cpx[pr][lane], 0u);
+            pc_publish(&ev[pr][1], ++cev);              // group done: ring, fin and cpos free
+            const uint64_t r = g * 64 + lane;
+            if (r < n) {
+                BRB_MetaDataUnpackInfo o;
+                o.error_code = code;
+                o.item_count = v[8];
+                o.cur_offset = uint64_t(v[9]) | (uint64_t(v[10]) << 32);
+                o.cur_remaining = uint64_t(v[11]) | (uint64_t(v[12]) << 32);
+                o.cur_needed = uint64_t(v[13]) | (uint64_t(v[14]) << 32);
+                info[r] = o;
+            }
+        }
+        return;
+    }
+
+    const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + pr * NS * kSlot;
     const uint64_t dbase = reinterpret_cast<uint64_t>(data);
+    uint32_t *const my_cpx = &cpx[PC ? pr : 0][lane];
+    uint32_t *const my_wpx = &wpx[PC ? pr : 0][lane];
     Win win;
     win.init(lane);
+    uint32_t pev = 0, cexp = 0;                         // pairs: events published, consumer events expected
 
-    for (uint64_t g = uint64_t(blockIdx.x) * W + wv; g < n_groups; g += uint64_t(gridDim.x) * W) {
+    for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
+        if (PC && !pc_wait_ge(&ev[pr][1], cexp))        // every earlier event acknowledged
+            return;
         const uint64_t r = g * 64 + lane;
         const bool valid = r < n;
         const uint64_t base = valid ? dbase + offs[r] : dbase;
@@ -217,11 +287,22 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         const uint32_t Kl = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
         const uint32_t K = Kl ? Kl : 1u;                  // iteration 1 reads every header
         brb_md5::FunnelT<RW> f;
-        f.init(&fring[wv][0][lane]);
+        f.init(&fring[pr][0][lane]);
         if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {   // no line, or too wide
+            if (PC) {                                     // the per-lane path, this wave only
+                ev[pr][2] = 0;
+                pc_publish(&ev[pr][0], ++pev);
+                cexp += 1;
+            }
             if (valid)
                 info[r] = unpack_lane(f, reinterpret_cast<const uint8_t *>(base), size);
             continue;
+        }
+        if (PC) {
+            *my_wpx = 0;                                  // the consumer reads it only after the plan
+            ev[pr][2] = K;
+            pc_publish(&ev[pr][0], ++pev);
+            cexp += 2;
         }
         const brb_dma::v4i rs = group_rsrc(lo, hi);
         const uint32_t rel0 = nl ? uint32_t(line0 - lo) : kOOB;
@@ -234,6 +315,7 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
         int32_t code = BRB_METADATA_UNPACK_SUCCESS, item_count = 0, item = 0;
         uint32_t items = 0, phase = kDone, b = 0, dig[4] = {0, 0, 0, 0};
         uint64_t offset = 0, remaining = 0, needed = 0, ds = 0, de = 0;
+        bool ok = true;
 
         // The walk's events whose first byte lies before pack byte L1, line k-1 = pack bytes [L0, L1)
         // in the window.  drain: after the last line, the events a pack shorter than its header
@@ -289,11 +371,7 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
                         Emit e;
                         plan_range(f, first, uint32_t(int64_t(ds) - L0), er < 4096 ? uint32_t(er) : 4096u, b, e);
                         edge_words(win, sa, sb, e);
-                        emit_half<RW, 0, false>(f, e, dw);
-                        pump_all(f);
-                        emit_half<RW, 1, false>(f, e, dw);
-                        emit_finish(f, e);
-                        pump_all(f);
+                        ok = emit_line<RW, false, PC>(f, e, dw, true, my_cpx, my_wpx) && ok;
                         done = !e.any || e.ends;
                     }
                     more = done;                                 // else the line is used up (no second emission)
@@ -351,25 +429,37 @@ __global__ __launch_bounds__(64 * W) void metadata_line_kernel(const uint8_t *__
             const bool whole = phase == kDone ||
                                (phase == kData && int64_t(ds) < L0 && int64_t(de) - L0 > 128 + int64_t(b));
             if (k > 1 && __builtin_amdgcn_ballot_w64(!whole) == 0) {
+                // line k+NS-1 into line k-1's slot at once: the emission reads the window registers only
+                issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + NS - 1), lane);
                 Emit e;
                 plan_whole(f, b, e);
-                if (phase == kData)
-                    emit_half<RW, 0, true>(f, e, dw);
-                pump_all(f);
-                if (phase == kData)
-                    emit_half<RW, 1, true>(f, e, dw);
-                pump_all(f);
+                ok = emit_line<RW, true, PC>(f, e, dw, phase == kData, my_cpx, my_wpx) && ok;
             } else {
                 events(L0, L0 + 128, lds0 + sa, lds0 + sb, dw, false);
+                // line k+NS-1 into line k-1's slot (its window reads are done)
+                issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + NS - 1), lane);
             }
-            // line k+NS-1 into line k-1's slot (its window reads are done)
-            issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + NS - 1), lane);
             sa = sb;
+            if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)
+                break;
         }
         brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
+        if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)
+            return;                                              // a protocol fault (wrong results, no hang)
         if (phase != kDone) {                                    // a pack shorter than its header
             uint32_t dw[36] = {};
             events(int64_t(1) << 62, int64_t(1) << 62, 0, 0, dw, true);
+        }
+        if (PC) {
+            const uint32_t v[15] = {uint32_t(f.acc) | (f.nacc << 24), uint32_t(f.total), uint32_t(f.total >> 32),
+                                    uint32_t(code), dig[0], dig[1], dig[2], dig[3], items,
+                                    uint32_t(offset), uint32_t(offset >> 32), uint32_t(remaining),
+                                    uint32_t(remaining >> 32), uint32_t(needed), uint32_t(needed >> 32)};
+#pragma unroll
+            for (int q = 0; q < 15; q++)
+                fin[pr][q][lane] = v[q];
+            pc_publish(&ev[pr][0], ++pev);                       // the group's end
+            continue;
         }
         if (!valid)
             continue;
@@ -401,16 +491,18 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
         metadata_unpack_kernel<<<unsigned((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(data, offs, lens, n, info);
         return hipGetLastError();
     }
-    constexpr int W = 4;                               // 4 x 32 KiB of LDS: one workgroup per CU
+    constexpr int W = 4;                               // 4 walking waves: one workgroup per CU
     const uint64_t groups = (n + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
+    if (brb_opt::get(brb_opt::kSegLine) == 2)          // wave pairs
+        metadata_line_kernel<W, 2, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info);
     // three slots by default: 43.6 vs 49.3 us with two (bench --op metadata, interleaved A/B,
     // gpurun_out/r04s_md); test option line_slots 2 for the other
-    if (brb_opt::get(brb_opt::kLineSlots) == 2)
-        metadata_line_kernel<W, 2><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+    else if (brb_opt::get(brb_opt::kLineSlots) == 2)
+        metadata_line_kernel<W, 2, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
     else
-        metadata_line_kernel<W, 3><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+        metadata_line_kernel<W, 3, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
     return hipGetLastError();
 }
 

@@ -18,14 +18,15 @@ enum Opt {
     kB64Group = 5,      // -1: the launcher's choice; 0..6: log2 of the base64 lanes per record
     kHostChunkMiB = 6,  // 0: host-mode Blowfish/RC4 chunks of 16 MiB; k: k MiB (tools/host_sweep.py)
     kHostDigestChunkMiB = 7,   // 0: host-mode digest chunks of 32 MiB; k: k MiB
-    kSegLine = 8,       // 1: segment digests / MetaData unpack on the line-staged kernels; 0: per-lane
+    kSegLine = 8,       // segment digests / MetaData unpack: 2 line-staged wave pairs (default), 1 line-staged
+                        // single waves, 0 the per-lane kernels
     kB64Kernel = 9,     // 64-byte fixed-stride records: 2 digest_b64r_kernel at 8 waves per SIMD (default), 3 the same
                         // at 4, 1 digest_b64_kernel (two LDS slots), 0 the generic DMA kernel
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
     kCount = 11
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 1, 2, 0};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

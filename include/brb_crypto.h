@@ -388,8 +388,8 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * caller order), "devices" 0/k (all-devices calls and batchers on every visible device / forced into k <= 16
  * parts, part g on device g % count; an all-devices batcher takes at most 16 parts either way), "b64_group" -1/0..6 (base64 lanes per record: launcher's choice /
  * forced to 2^value), "host_chunk_mib" / "host_digest_chunk_mib" 0/k (host-mode chunks of the default
- * 16 / 32 MiB, or k MiB; chunk-size sweeps), "seg_line" 1/0 (segment digests and MetaData unpack on the
- * line-staged kernels / the per-lane kernels), "b64_kernel" 2/3/1/0 (64-byte fixed-stride records on
+ * 16 / 32 MiB, or k MiB; chunk-size sweeps), "seg_line" 2/1/0 (segment digests and MetaData unpack on the
+ * line-staged producer / consumer wave pairs, the line-staged single waves, the per-lane kernels), "b64_kernel" 2/3/1/0 (64-byte fixed-stride records on
  * the register-buffered kernel at 8 / 4 waves per SIMD, the two-slot kernel, the generic one),
  * "line_slots" 0/2/3 (LDS-DMA ring slots of the line-staged segment and MetaData kernels: each
  * kernel's default, or forced).  Returns 1 and the previous

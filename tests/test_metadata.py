@@ -157,10 +157,10 @@ def infos_as_tuples(info):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seg_line,slots", [(1, 3), (1, 2), (0, 0)])
+@pytest.mark.parametrize("seg_line,slots", [(1, 3), (1, 2), (2, 0), (0, 0)])
 def test_unpack_batch_vs_oracle(brb, orc, seg_line, slots):
     """seg_line 1: the line-staged kernel (round 4) with `slots` LDS-DMA ring slots (test option
-    line_slots), 0: the per-lane kernel."""
+    line_slots), 2: its producer / consumer wave-pair form, 0: the per-lane kernel."""
     packs = corpus(3, 4000)
     rng = np.random.default_rng(4)
     buf, offs, lens = scatter(rng, packs)
@@ -178,7 +178,7 @@ def test_unpack_batch_vs_oracle(brb, orc, seg_line, slots):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seg_line", [1, 0])
+@pytest.mark.parametrize("seg_line", [1, 2, 0])
 def test_unpack_batch_bench_count(brb, orc, seg_line):
     """A bench-sized batch: 65 536 valid and mutated packs (every return code) at arbitrary byte
     offsets, device mode, every BRB_MetaDataUnpackInfo field against the oracle."""
@@ -196,8 +196,9 @@ def test_unpack_batch_bench_count(brb, orc, seg_line):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seg_line", [1, 2])
 @pytest.mark.parametrize("n_items,item_len,gap", [(4, 375, 0), (9, 61, 3), (40, 2, 1), (2, 1000, 77), (13, 0, 5)])
-def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap):
+def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap, seg_line):
     """Batches whose packs share one layout (the bench's 4 x 375-byte items, and tiny / empty /
     large items), so every lane of a wave reaches its events in the same line; packs back to back
     or with `gap` bytes between them; 20 % carry a flipped byte; every field vs the oracle."""
@@ -216,7 +217,8 @@ def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap):
         pos += len(p) + gap
     buf = np.frombuffer(b"".join(parts) + b"\0", np.uint8).copy()
     lens = np.array([len(p) for p in packs], np.uint32)
-    got = infos_as_tuples(brb.metadata_unpack_batch(buf, np.array(offs, np.uint64), lens))
+    with brb.TestOption("seg_line", seg_line):
+        got = infos_as_tuples(brb.metadata_unpack_batch(buf, np.array(offs, np.uint64), lens))
     assert got == [orc.metadata_unpack(p) for p in packs]
 
 
@@ -236,7 +238,7 @@ def test_pack_batch_round_trip(brb, orc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seg_line", [1, 0])
+@pytest.mark.parametrize("seg_line", [1, 2, 0])
 def test_unpack_large_items(brb, orc, seg_line):
     """Items of 64 KiB .. 1 MiB (many MD5 blocks per lane, items spanning block boundaries at every
     byte offset) next to tiny packs in the same batch."""
@@ -253,7 +255,8 @@ def test_unpack_large_items(brb, orc, seg_line):
 
 
 @pytest.mark.gpu
-def test_unpack_beyond_4gib(brb, orc):
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_unpack_beyond_4gib(brb, orc, seg_line):
     """Packs at byte offsets past 2^32: the same 2 000 scattered packs copied into one 4.5 GiB
     device buffer three times -- straddling 2^31, straddling 2^32, and ending at the buffer's last
     byte -- and unpacked in one call; every BRB_MetaDataUnpackInfo field equals the oracle's."""
@@ -274,7 +277,8 @@ def test_unpack_beyond_4gib(brb, orc):
     assert int((all_offs + all_lens).max()) <= total
     o = torch.from_numpy(all_offs.view(np.int64)).cuda()
     ln = torch.from_numpy(all_lens.view(np.int32)).cuda()
-    dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    with brb.TestOption("seg_line", seg_line):
+        dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
     assert infos_as_tuples(dev) == want * 3
     del d, src
     torch.cuda.empty_cache()
