@@ -169,9 +169,9 @@ ISSUE_CYC_W2 = 4.05    # per SIMD with two or more waves sharing it (the MD5 mix
 
 
 def issue_compute(path, key, launch_s, dispatches=1):
-    """roofline.compute for the lines that run one wave per SIMD and are bound by that wave's
-    instruction issue rather than by HBM (RC4 and frame/open, MetaData unpack, segment digests,
-    variable-length digests).  From the kept --pmc pass of the same kernel
+    """roofline.compute for the lines bound by instruction issue rather than by HBM: one wave per
+    SIMD (RC4 and frame/open, variable-length digests) or one producer / consumer wave pair per
+    SIMD (MetaData unpack, segment digests; both waves' instructions count); VERDICT r03 item 4.  From the kept --pmc pass of the same kernel
     (per dispatch; `dispatches` per step):
       issued_per_simd  (SQ_INSTS_VALU + SQ_INSTS_LDS + SQ_INSTS_SALU) / 1024 SIMDs
       frac_issue_ceiling  issued_per_simd x cycles per instruction / (launch time x CLOCK_GHZ): the
