@@ -26,6 +26,7 @@
 
 #include "digest_line.h"
 #include "md5_funnel.h"
+#include "pair_sync.h"
 
 namespace brb_line {
 
@@ -278,32 +279,9 @@ BRB_DEV void emit_finish(brb_md5::FunnelT<RW> &f, const Emit &p)
     }
 }
 
-// ---- producer / consumer wave pairs (md5_seg_pc_kernel, metadata_pc_kernel) ------------------
+// ---- producer / consumer wave pairs (md5_seg_pc_kernel, metadata_line_kernel<..., PC>) ----------
 // A pair's two waves share a funnel ring: the producer stages lines and emits message words, the
-// consumer compresses them.  Each publishes a running event count in LDS (one writer per counter,
-// release store after its ring / table writes; the reader's acquire load orders its reads after).
-// Every wait is bounded (~2^22 sleeps, far beyond any launch): a protocol fault ends the launch
-// with wrong digests, never a hung wave.
-BRB_DEV bool pc_wait_ge(uint32_t *ctr, uint32_t target)
-{
-    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-        const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__builtin_amdgcn_readfirstlane(v) >= target)
-            return true;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
-{
-    __hip_atomic_store(ctr, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-BRB_DEV uint32_t pc_load(uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+// consumer compresses them (pair_sync.h for the hand-off primitives).
 
 // Producer side, per lane: wait until the lane's ring has room for a half-line of words (at most
 // 17, plus the free slot past them that emit_half's clamp may write): wpos - cpos <= RW - 18, cpos

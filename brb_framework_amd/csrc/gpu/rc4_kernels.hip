@@ -13,6 +13,7 @@
 #include <type_traits>
 
 #include "brb_kernels.h"
+#include "pair_sync.h"
 #include "rc4_device.h"
 #include "test_options.h"
 
@@ -319,6 +320,169 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     g.store(state);
 }
 
+// RC4 + MD5 wave pairs for the read side (round 4).  rc4md5_open_kernel runs one wave per SIMD
+// (65 536 connections = 1 024 waves) whose keystream steps wait on LDS round trips: the SIMD issues
+// in ~59 % of the launch's cycles (roofline.compute.issue_busy_frac of the rc4md5 line), and the
+// MD5 of the decrypted payload sits on that wave's instruction stream.  rc4md5_open_pair_kernel
+// gives a workgroup the 4 RC4 waves of 256 connections and 4 MD5 waves for the same connections
+// (wave w + 4 beside wave w): the RC4 wave decrypts and drops each MD5 block's 16 message words into
+// a 32-word per-lane LDS ring, posting its count (wpx); the MD5 wave compresses them as they come
+// and posts its own count (cpx).  The RC4 wave writes a block only while the ring has room (block
+// b - 2 compressed) and keeps the SIMD's issue priority: its chain is the critical path.
+// Interleaved rocprofv3 A/B (65 536 x 1 530-byte frames): open 122.9 -> 111.9 us.  The write side
+// measured no gain as a pair (frame 128.1 -> 127.2 us with the payload words passed through the ring,
+// 132.3 us with wave-cooperative loads, 155.9 us with the MD5 wave loading the payload itself): its
+// RC4 wave alone takes as long as the fused kernel, so the frame kernel stays single.
+struct PairRing {
+    uint32_t (*ring)[64];   // [32][64]: word k of lane l at ring[k % 32][l]
+    uint32_t *wpx, *cpx;    // this lane's mailboxes
+    uint32_t lane;
+
+    // RC4 wave: MD5 block b's words into the ring once block b - 2 is compressed; false on a fault
+    BRB_DEV bool put(uint64_t b, const uint32_t (&m)[16]) const
+    {
+        bool room = false;
+        for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+            if (__builtin_amdgcn_ballot_w64(uint64_t(brb_line::pc_load(cpx)) + 32 < 16 * (b + 1)) == 0) {
+                room = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t q = uint32_t(b & 1) * 16;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            ring[q + i][lane] = m[i];
+        brb_line::pc_publish(wpx, uint32_t(16 * (b + 1)));
+        return room;
+    }
+    // MD5 wave: block b's words once posted; false on a fault
+    BRB_DEV bool get(uint64_t b, uint32_t (&m)[16]) const
+    {
+        bool in = false;
+        for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+            if (__builtin_amdgcn_ballot_w64(brb_line::pc_load(wpx) < 16 * (b + 1)) == 0) {
+                in = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t q = uint32_t(b & 1) * 16;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            m[i] = ring[q + i][lane];
+        return in;
+    }
+    BRB_DEV void done(uint64_t b) const { brb_line::pc_publish(cpx, uint32_t(16 * (b + 1))); }
+};
+
+// The read side as a pair: the RC4 wave decrypts the frame as rc4md5_open_kernel does and drops each
+// MD5 block's 16 payload words (two frame blocks funnel-shifted by 2 bytes) into the ring; the MD5
+// wave compresses them, pads, compares the digest with the decrypted header (posted with block 0)
+// and writes the valid flag.
+__global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__restrict__ states, const uint8_t *in,
+                                                                     uint8_t *out, const uint64_t *__restrict__ offs,
+                                                                     const uint32_t *__restrict__ lens, uint64_t n,
+                                                                     uint8_t *__restrict__ valid,
+                                                                     const uint32_t *__restrict__ sidx,
+                                                                     const uint64_t *__restrict__ ooffs)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    __shared__ uint32_t ring[kWaves][32][64];
+    __shared__ uint32_t hdr[kWaves][6][64];       // decrypted header chunks 2..7
+    __shared__ uint32_t wpx[kWaves][64], cpx[kWaves][64];
+    __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w4 = wv % kWaves;
+    if (threadIdx.x < kWaves * 64) {
+        (&wpx[0][0])[threadIdx.x] = 0;
+        (&cpx[0][0])[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const PairRing pr{ring[w4], &wpx[w4][lane], &cpx[w4][lane], lane};
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
+    if (wv >= kWaves) {
+        if (s >= n)
+            return;
+        const uint64_t F = lens[s];
+        // ---- MD5 wave (EvAIOReqTransform_RC4_MD5_DataValidate, ev_kq_aio_transform.c:158-184)
+        uint32_t ok = 0;
+        if (F >= kHeader) {
+            const uint64_t len = F - kHeader;
+            const uint64_t nblk = md5_blocks(len), nw = 16 * nblk;
+            Md5State st = md5_iv();
+            bool in = true;
+            for (uint64_t b = 0; b < nblk && in; b++) {
+                uint32_t m[16];
+                in = pr.get(b, m);
+                md5_pad_block(m, b, len, nw);
+                md5_compress(st, m);
+                pr.done(b);
+            }
+            const uint32_t h2 = hdr[w4][0][lane], h3 = hdr[w4][1][lane], h4 = hdr[w4][2][lane],
+                           h5 = hdr[w4][3][lane], h6 = hdr[w4][4][lane], h7 = hdr[w4][5][lane];
+            const bool tag = h2 == 0x48534148u && (h3 & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
+            const bool dig = __builtin_amdgcn_alignbit(h4, h3, 8) == st.a && __builtin_amdgcn_alignbit(h5, h4, 8) == st.b &&
+                             __builtin_amdgcn_alignbit(h6, h5, 8) == st.c && __builtin_amdgcn_alignbit(h7, h6, 8) == st.d;
+            ok = tag && dig && in;
+        }
+        valid[s] = uint8_t(ok);
+        return;
+    }
+    // ---- RC4 wave (issue priority: its chain is the critical path; wave-cooperative loads)
+    __builtin_amdgcn_s_setprio(3);
+    const bool live = s < n;
+    Gen g;
+    g.P.lds = slot;
+    g.P.lw = lane * 4 + w4;
+    uint8_t *state = nullptr;
+    uint64_t off = 0, F = 0;
+    if (live) {
+        state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;
+        g.load(state);
+        off = offs[s];
+        F = lens[s];
+    }
+    brb_io::BlockSrcW src;
+    Snk snk;
+    src.init(in + off, F, xch + w4 * kXchBytes);
+    snk.init(out + (live && ooffs ? ooffs[s] : off), F);
+    uint32_t cur[16], c[16];
+    src.fetch(c);
+    if (live)
+        decrypt_block(c, snk, g, F, 0, cur);
+    const bool framed = live && F >= kHeader;
+    if (framed) {
+#pragma unroll
+        for (int q = 0; q < 6; q++)
+            hdr[w4][q][lane] = cur[2 + q];        // read by the MD5 wave after the first post
+    }
+    const uint64_t nblk = framed ? md5_blocks(F - kHeader) : 0;
+    const uint32_t nloop = wave_max(uint32_t(nblk));
+    for (uint32_t b = 0; b < nloop; b++) {
+        src.fetch(c);
+        if (b >= nblk)
+            continue;
+        uint32_t nxt[16], m[16];
+        decrypt_block(c, snk, g, F, b + 1, nxt);
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const uint32_t lo = i + 7 < 16 ? cur[i + 7] : nxt[i - 9];
+            const uint32_t hi = i + 8 < 16 ? cur[i + 8] : nxt[i - 8];
+            m[i] = __builtin_amdgcn_alignbit(hi, lo, 16);
+        }
+        pr.put(b, m);                             // a fault shows as an invalid frame (the MD5 wave's get)
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            cur[i] = nxt[i];
+    }
+    if (!live)
+        return;
+    snk.flush();
+    g.store(state);
+}
+
 inline unsigned grid_for(uint64_t n) { return unsigned((n + kWave - 1) / kWave); }
 
 }  // namespace
@@ -358,7 +522,10 @@ hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, 
 {
     if (n == 0)
         return hipSuccess;
-    rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
+    if (brb_opt::get(brb_opt::kRc4Pair) != 0)
+        rc4md5_open_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
+    else
+        rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
     return hipGetLastError();
 }
 

@@ -23,10 +23,11 @@ enum Opt {
     kB64Kernel = 9,     // 64-byte fixed-stride records: 2 digest_b64r_kernel at 8 waves per SIMD (default), 3 the same
                         // at 4, 1 digest_b64_kernel (two LDS slots), 0 the generic DMA kernel
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
-    kCount = 11
+    kRc4Pair = 11,      // 1: RC4+MD5 open on RC4 + MD5 wave pairs (default); 0: one wave does both
+    kCount = 12
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

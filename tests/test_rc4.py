@@ -223,9 +223,17 @@ def _oracle_frames(orc, states, payload, offs, lens, salts, frames, foffs):
     return st, fr
 
 
+@pytest.fixture(params=[1, 0], ids=["pair", "single"])
+def rc4md5_pair(request, brb):
+    """Test option rc4md5_pair: 1 the RC4 + MD5 wave-pair open kernel (default), 0 one wave doing both
+    (the frame kernel is the same either way)."""
+    with brb.TestOption("rc4md5_pair", request.param):
+        yield request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fbase", [0, 1, 2, 3])
-def test_rc4md5_frame_batch(brb, orc, torch_dev, fbase):
+def test_rc4md5_frame_batch(brb, orc, torch_dev, fbase, rc4md5_pair):
     lens = (RAGGED * 4)[: 100]
     offs, lens, total = _layout(lens, 3, 1)
     payload = workload.gen_records(SEED, 7, 1, total + 4)
@@ -260,7 +268,7 @@ def test_rc4md5_golden_frames(brb, golden):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("base", [0, 1, 2, 3])
-def test_rc4md5_open_batch(brb, orc, torch_dev, base):
+def test_rc4md5_open_batch(brb, orc, torch_dev, base, rc4md5_pair):
     """Frames written by the oracle are opened on the GPU; corrupted / short frames are rejected."""
     lens = (RAGGED * 4)[: 108]
     keys = _keys(len(lens), 12)
@@ -306,7 +314,7 @@ def test_rc4md5_open_batch(brb, orc, torch_dev, base):
 
 
 @pytest.mark.gpu
-def test_rc4md5_round_trip_large(brb, torch_dev):
+def test_rc4md5_round_trip_large(brb, torch_dev, rc4md5_pair):
     """Frame on the GPU, open on the GPU: 4096 connections x 1500 B plus a few 64 KiB payloads."""
     torch = torch_dev
     lens = [1500] * 4096 + [65536, 65535, 65537]
