@@ -341,20 +341,28 @@ BRB_DEV bool emit_line(brb_md5::FunnelT<RW> &f, Emit &e, const uint32_t (&dw)[36
 
 // Consumer: compresses the lane's words as the producer posts them (wpx), posting its own count
 // (cpx), until the producer's event count reaches `end` (its last post is in by then).  False when
-// the producer never got there (a protocol fault; the launch's digests are then wrong, but it ends).
+// the producer stopped (2^22 sleeps with no word, no end and no beat of hb: a protocol fault; the
+// launch's digests are then wrong, but it ends).
 template <uint32_t RW>
 BRB_DEV bool pc_consume(brb_md5::FunnelT<RW> &f, uint32_t *ev_p, uint32_t end, uint32_t *wpx, uint32_t *cpx,
-                        uint64_t *idle = nullptr)
+                        uint32_t *hb, uint64_t *idle = nullptr)
 {
-    for (uint32_t spin = 0; spin < (1u << 24); spin++) {
+    uint32_t last = pc_beat_of(hb);
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
         const bool ended = __builtin_amdgcn_readfirstlane(pc_load(ev_p)) >= end;   // before wpos: the last post is in
         f.wpos = pc_load(wpx);
         if (__builtin_amdgcn_ballot_w64(f.wpos - f.cpos >= 16) != 0) {
             pump_all(f);
             pc_publish(cpx, f.cpos);
+            spin = 0;
         } else if (ended) {
             return true;
         } else {
+            const uint32_t h = pc_beat_of(hb);
+            if (h != last) {
+                last = h;
+                spin = 0;
+            }
             const uint64_t t = idle ? __builtin_amdgcn_s_memtime() : 0;
             __builtin_amdgcn_s_sleep(1);
             if (idle)

@@ -23,9 +23,9 @@ constexpr int kBlock = 256;
 // mod 4 bytes before it, so its words fall on the digest's word boundaries (Funnel::head); those e
 // bytes are the carried ones, never loaded from below the segment.  Used for groups whose lines span
 // 2 GiB or more, and by the round-3 kernel kept for A/B (test option seg_line = 0).
-template <uint32_t RW>
+template <uint32_t RW, class Beat = brb_line::NoBeat>
 BRB_DEV void seg_lane(brb_md5::FunnelT<RW> &f, const uint8_t *__restrict__ data, const uint64_t *__restrict__ soff,
-                      const uint32_t *__restrict__ slen, uint64_t k, uint64_t k1)
+                      const uint32_t *__restrict__ slen, uint64_t k, uint64_t k1, Beat beat = Beat())
 {
     uint64_t before = 0;
     auto skip_empty = [&](uint64_t kk) {                // the next segment with bytes (an empty one's
@@ -53,6 +53,7 @@ BRB_DEV void seg_lane(brb_md5::FunnelT<RW> &f, const uint8_t *__restrict__ data,
             else
                 f.put_tail(w, uint32_t(left));
             f.pump();
+            beat();
         }
         if ((n & 63) == 0) {                            // ended on a whole block: nothing carried
             f.acc = 0;
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     __shared__ uint32_t tab_len[NP][kTab];
     __shared__ uint32_t wpx[NP][64], cpx[NP][64];       // the mailboxes: words written, words compressed
     __shared__ uint32_t fin[NP][3][64];                 // carried bytes | count << 24, length lo / hi
-    __shared__ uint32_t ev[NP][4];                      // producer events, consumer events, plan
+    __shared__ uint32_t ev[NP][4];                      // producer events, consumer events, plan, heartbeat
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pr = wv % NP;
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         const uint64_t c_t0 = __builtin_amdgcn_s_memtime();
 #endif
         for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
-            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3]))
                 return;
             pseen++;
             const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
@@ -380,10 +381,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
 #ifdef BRB_LINE_STAMPS
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &c_wait))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3], &c_wait))
                 return;
 #else
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane]))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3]))
                 return;
 #endif
             pseen++;
@@ -415,6 +416,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     Win win;
     win.init(lane);
     uint32_t pev = 0, cexp = 0;                         // events published; consumer events expected so far
+    uint32_t beats = 0;                                 // heartbeat: one per line
 #ifdef BRB_LINE_STAMPS    // the producer's waits for ring room and for its DMA
     uint64_t p_wait = 0, p_dma = 0;
     const uint64_t p_t0 = __builtin_amdgcn_s_memtime();
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             pc_publish(&ev[pr][0], ++pev);
             cexp += 1;
             if (valid) {
-                seg_lane(f, data, soff, slen, k0, k1);
+                seg_lane(f, data, soff, slen, k0, k1, brb_line::HbBeat{&ev[pr][3], 0});
                 store_digest(out, rec, f.finish());
             }
         };
@@ -543,6 +545,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
                 ok = false;
                 break;
             }
+            pc_beat(&ev[pr][3], ++beats);
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                       // the stray stage past K, before the slots are reused

@@ -65,8 +65,9 @@ struct Ahead {
 // MetaDataUnpack of one pack by one lane with per-lane loads (the round-3 kernel's walk): groups
 // whose packs span 2 GiB or more take it inside the line-staged kernel, and the round-3 kernel
 // (test option seg_line = 0) is this function per lane.
-template <uint32_t RW>
-BRB_DEV BRB_MetaDataUnpackInfo unpack_lane(brb_md5::FunnelT<RW> &f, const uint8_t *base, uint64_t size)
+template <uint32_t RW, class Beat = brb_line::NoBeat>
+BRB_DEV BRB_MetaDataUnpackInfo unpack_lane(brb_md5::FunnelT<RW> &f, const uint8_t *base, uint64_t size,
+                                           Beat beat = Beat())
 {
     int32_t code;
     uint32_t items = 0;
@@ -121,6 +122,7 @@ BRB_DEV BRB_MetaDataUnpackInfo unpack_lane(brb_md5::FunnelT<RW> &f, const uint8_
                 else
                     f.put_tail(w, uint32_t(left));
                 f.pump();
+                beat();
             }
             if ((n & 63) == 0) {                            // ended on a whole block: nothing carried
                 f.acc = 0;
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
     __shared__ __attribute__((aligned(RW * 256))) uint32_t fring[W][RW][64];
     __shared__ uint32_t wpx[WP][64], cpx[WP][64];       // pairs: words written, words compressed
     __shared__ uint32_t fin[WP][15][64];                // pairs: the walk's results for the consumer
-    __shared__ uint32_t ev[WP][4];                      // pairs: producer events, consumer events, plan
+    __shared__ uint32_t ev[WP][4];                      // pairs: producer events, consumer events, plan, heartbeat
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pr = PC ? wv % W : wv;
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
         // ---------------- consumer ----------------
         uint32_t pseen = 0, cev = 0;
         for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
-            if (!pc_wait_ge(&ev[pr][0], pseen + 1))
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3]))
                 return;
             pseen++;
             const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
                 continue;                               // the producer runs this group alone
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane]))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3]))
                 return;
             pseen++;
             uint32_t v[15];
@@ -271,6 +273,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
     Win win;
     win.init(lane);
     uint32_t pev = 0, cexp = 0;                         // pairs: events published, consumer events expected
+    uint32_t beats = 0;                                 // pairs: heartbeat, one per line
 
     for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
         if (PC && !pc_wait_ge(&ev[pr][1], cexp))        // every earlier event acknowledged
@@ -294,8 +297,12 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
                 pc_publish(&ev[pr][0], ++pev);
                 cexp += 1;
             }
-            if (valid)
-                info[r] = unpack_lane(f, reinterpret_cast<const uint8_t *>(base), size);
+            if (valid) {
+                if (PC)
+                    info[r] = unpack_lane(f, reinterpret_cast<const uint8_t *>(base), size, brb_line::HbBeat{&ev[pr][3], 0});
+                else
+                    info[r] = unpack_lane(f, reinterpret_cast<const uint8_t *>(base), size);
+            }
             continue;
         }
         if (PC) {
@@ -440,8 +447,11 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
                 issue_rows(rs, lds0 + sa, phase == kDone ? kOOB : line_rel(k + NS - 1), lane);
             }
             sa = sb;
-            if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)
-                break;
+            if (PC) {
+                pc_beat(&ev[pr][3], ++beats);
+                if (__builtin_amdgcn_ballot_w64(!ok) != 0)
+                    break;
+            }
         }
         brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
         if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)

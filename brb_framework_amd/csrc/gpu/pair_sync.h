@@ -2,20 +2,56 @@
 // (md5_seg_pc_kernel, metadata_line_kernel<..., PC>, the RC4+MD5 frame / open pairs).
 // One writer per counter or mailbox: release store after the data it covers, acquire load before
 // the reads it guards (workgroup scope: both waves are in one workgroup, so LDS and the CU's L1 are
-// shared).  Every wait is bounded (~2^22 sleeps, far beyond any launch): a protocol fault gives
-// wrong results, never a hung wave.
+// shared).  Every wait is bounded (~2^22 sleeps without progress from the other wave): a protocol
+// fault gives wrong results, never a hung wave.
 #pragma once
 
 #include "brb_gpu_common.h"
 
 namespace brb_line {
 
-BRB_DEV bool pc_wait_ge(uint32_t *ctr, uint32_t target)
+BRB_DEV uint32_t pc_load(uint32_t *p)
 {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// A heartbeat: the working wave bumps it as it goes (no ordering needed, so a relaxed store: no
+// wait for its own LDS writes), and a waiting wave's budget counts only sleeps with no beat.  So a
+// legitimately long stretch (a lane's multi-GiB record on the per-lane path, thousands of lines of
+// empty items) never times out, while a wave whose partner stopped still ends.
+BRB_DEV void pc_beat(uint32_t *hb, uint32_t v)
+{
+    __hip_atomic_store(hb, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+BRB_DEV uint32_t pc_beat_of(uint32_t *hb)
+{
+    return hb ? __builtin_amdgcn_readfirstlane(__hip_atomic_load(hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) : 0u;
+}
+
+// Per-block beat hooks for code shared with the single-wave kernels (seg_lane, unpack_lane).
+struct NoBeat {
+    BRB_DEV void operator()() {}
+};
+struct HbBeat {
+    uint32_t *hb;
+    uint32_t n;
+    BRB_DEV void operator()() { pc_beat(hb, ++n); }
+};
+
+// Waits until *ctr >= target; false after 2^22 sleeps without a beat of *hb (if given).
+BRB_DEV bool pc_wait_ge(uint32_t *ctr, uint32_t target, uint32_t *hb = nullptr)
+{
+    uint32_t last = pc_beat_of(hb);
     for (uint32_t spin = 0; spin < (1u << 22); spin++) {
         const uint32_t v = __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (__builtin_amdgcn_readfirstlane(v) >= target)
             return true;
+        const uint32_t h = pc_beat_of(hb);
+        if (h != last) {
+            last = h;
+            spin = 0;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
     return false;
@@ -26,9 +62,5 @@ BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
     __hip_atomic_store(ctr, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-BRB_DEV uint32_t pc_load(uint32_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 }  // namespace brb_line

@@ -256,6 +256,45 @@ def test_unpack_large_items(brb, orc, seg_line):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seg_line", [1, 2])
+def test_unpack_long_stretches(brb, orc, seg_line):
+    """Work that outlasts a wait without progress: (1) a pack of 300 000 empty items (8 MB, tens of
+    thousands of lines in which the walk emits no message word) beside ordinary packs, and (2) a
+    64 MiB item in a pack placed more than 2 GiB from its group's other packs (the per-lane path,
+    the producer alone while its partner waits for the next plan).  Every field vs the oracle."""
+    import torch
+    rng = np.random.default_rng(23)
+    empty = build([(i & 0xFF, 1, b"") for i in range(300_000)])
+    small = [build([(1, 2, rng.integers(0, 256, 300, dtype=np.uint8).tobytes())]) for _ in range(70)]
+    huge = build([(3, 4, rng.integers(0, 256, 64 << 20, dtype=np.uint8).tobytes())])
+    packs = [empty] + small[:63] + [huge] + small[63:]
+    far = (1 << 31) + 12345
+    total = far + len(huge) + 64
+    d = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    offs, pos = [], 0
+    for i, p in enumerate(packs):
+        if p is huge:
+            o = far
+        else:
+            o = pos
+            pos += len(p) + 3
+        offs.append(o)
+        d[o:o + len(p)] = torch.from_numpy(np.frombuffer(p, np.uint8).copy()).cuda()
+    assert pos < far
+    offs = np.array(offs, np.uint64)
+    lens = np.array([len(p) for p in packs], np.uint32)
+    o = torch.from_numpy(offs.view(np.int64)).cuda()
+    ln = torch.from_numpy(lens.view(np.int32)).cuda()
+    with brb.TestOption("seg_line", seg_line):
+        dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    want = [orc.metadata_unpack(p) for p in packs]
+    assert infos_as_tuples(dev) == want
+    assert want[0][0] == want[64][0] == 7                  # both long packs unpack (METADATA_UNPACK_SUCCESS)
+    del d
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_line", [1, 2])
 def test_unpack_beyond_4gib(brb, orc, seg_line):
     """Packs at byte offsets past 2^32: the same 2 000 scattered packs copied into one 4.5 GiB
     device buffer three times -- straddling 2^31, straddling 2^32, and ending at the buffer's last

@@ -137,6 +137,37 @@ def test_segments_mixed_wide_groups(brb, torch_dev, seg_line):
     t.cuda.empty_cache()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_long_lane_in_wide_group(brb, torch_dev, seg_line):
+    """A group whose lines span more than 2 GiB takes the per-lane path (in the wave-pair kernel: the
+    producer alone, its partner waiting for the next plan); one of its lanes digests a 96 MiB segment
+    -- far longer than a wait without progress may last -- so the waiting wave must see the
+    producer's heartbeat.  128 records: group 0 wide with the long lane, group 1 ordinary."""
+    t = torch_dev
+    far = (1 << 31) + 4099
+    big = 96 << 20
+    d = t.empty(far + big + 4096, dtype=t.uint8, device="cuda")
+    g = t.Generator(device="cuda")
+    g.manual_seed(0x10C)
+    d.view(t.int64)[: (far + big + 4096) // 8].random_(generator=g)
+    n = 128
+    first = np.arange(n + 1, dtype=np.uint64) * 2
+    offs = (np.arange(2 * n, dtype=np.uint64) * 1000).astype(np.uint64)
+    lens = np.full(2 * n, 700, np.uint32)
+    offs[1], lens[1] = far, big                 # record 0: one segment past 2 GiB, 96 MiB long
+    offs[3] = far + 5                           # record 1 too: the group spans > 2 GiB
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(d, dev(offs), dev(lens), dev(first)).cpu().numpy()
+    for i in list(range(0, 4)) + [64, 100, 127]:
+        msg = b"".join(d[int(offs[k]):int(offs[k]) + int(lens[k])].cpu().numpy().tobytes()
+                       for k in range(int(first[i]), int(first[i + 1])))
+        assert got[i].tobytes() == hashlib.md5(msg).digest(), i
+    del d
+    t.cuda.empty_cache()
+
+
 def test_segments_equal_streaming_oracle(brb, orc):
     """The oracle's BRB_MD5Init/UpdateBig/Final restatement over the items = the batch digest."""
     import ctypes
