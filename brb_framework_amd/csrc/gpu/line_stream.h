@@ -251,9 +251,10 @@ BRB_DEV void emit_half(brb_md5::FunnelT<RW> &f, Emit &p, const uint32_t (&dw)[36
 {
     constexpr int lo = H ? 16 : -1, hi = H ? 32 : 16;
     constexpr uint32_t M = brb_md5::FunnelT<RW>::kMask;
-    // words written after this half: [i0, min(iw, hi)); the first slot after them
+    // words written after this half: [i0, min(iw, hi)); the first slot after them (a whole line:
+    // words 0 .. 31, so 16 after the first half and 32 after the second)
     const int top = p.iw < hi ? p.iw : hi;
-    const uint32_t n = uint32_t(top > p.i0 ? top - p.i0 : 0);
+    const uint32_t n = WHOLE ? uint32_t(H ? 32 : 16) : uint32_t(top > p.i0 ? top - p.i0 : 0);
     const uint32_t ahi = p.alo + (n << 8);
 #pragma unroll
     for (int i = lo; i < hi; i++) {
