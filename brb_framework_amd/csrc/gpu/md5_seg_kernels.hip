@@ -106,6 +106,86 @@ __global__ __launch_bounds__(kBlock) void md5_seg_kernel(const uint8_t *__restri
     store_digest(out, r, f.finish());
 }
 
+// A group's segments in the wave's LDS table, and its line plan (both line-staged kernels).  The
+// group's segments are one contiguous range of the arrays (first[] is monotone): [s0, s1).  They go
+// to the table with coalesced loads, so the stage cursor reads them with LDS latency and no
+// vector-memory load ever sits between a wave's DMA issues (a per-lane load there made hipcc wait
+// for it right before the DMA).  plan() is false when the group takes the per-lane path: more
+// segments than the table holds, no line at all, or lines spanning 2 GiB or more (32-bit voffsets).
+template <uint32_t kTab>
+struct SegGroup {
+    uint64_t *off;          // this wave's table
+    uint32_t *len;
+    uint32_t t0, t1;        // the lane's entries
+    uint32_t K;             // stages of the group's longest lane (an empty segment costs one)
+    uint64_t lo, hi;        // the group's 128-byte-aligned line span
+
+    BRB_DEV bool plan(const uint64_t *__restrict__ soff, const uint32_t *__restrict__ slen, uint64_t k0, uint64_t k1,
+                      bool valid, uint64_t dbase, uint32_t lane)
+    {
+        const uint64_t s0 = brb_digest::uniform64(brb_digest::wave_min64(valid ? k0 : ~uint64_t(0)));
+        const uint64_t s1 = brb_digest::uniform64(brb_digest::wave_max64(valid ? k1 : 0));
+        const uint64_t S = s1 > s0 ? s1 - s0 : 0;
+        if (S > kTab)
+            return false;
+        for (uint32_t i = lane; i < uint32_t(S); i += 64) {
+            off[i] = soff[s0 + i];
+            len[i] = slen[s0 + i];
+        }
+        __builtin_amdgcn_s_waitcnt(0);                  // the table is in LDS, every load of it done
+        __builtin_amdgcn_wave_barrier();
+        t0 = uint32_t(k0 - (valid ? s0 : k0));
+        t1 = uint32_t(k1 - (valid ? s0 : k1));
+        uint64_t l = ~uint64_t(0), h = 0;
+        uint32_t nl = 0;
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t n = len[t];
+            if (!n) {
+                nl++;
+                continue;
+            }
+            const uint64_t a = dbase + off[t];
+            const uint64_t l0 = a & ~uint64_t(127), l1 = (a + n + 127) & ~uint64_t(127);
+            l = l0 < l ? l0 : l;
+            h = l1 > h ? l1 : h;
+            nl += uint32_t((l1 - l0) >> 7);
+        }
+        lo = brb_digest::uniform64(brb_digest::wave_min64(l));
+        hi = brb_digest::uniform64(brb_digest::wave_max64(h));
+        K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
+        return hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16);   // K >= 1 then
+    }
+};
+
+// Stage cursor over a lane's segments: the line to stage next (offset from the group's lowest line;
+// kEnd: the cursor must enter the next segment first) and its segment; nt = the next table entry.
+struct SegCursor {
+    static constexpr uint32_t kEnd = 0xFFFFFFFFu;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint64_t base;          // dbase - lo
+    uint32_t nt, t1;
+    uint32_t c_line = kEnd, c_last = 0, c_ss = 0, c_se = 0;
+
+    BRB_DEV brb_line::LineDesc next()                   // this stage's line; the cursor moves on
+    {
+        if (c_line == kEnd && nt < t1) {                // enter segment nt
+            const uint32_t n = len[nt];
+            if (n) {
+                c_ss = uint32_t(base + off[nt]);
+                c_se = c_ss + n;
+                c_line = c_ss & ~127u;
+                c_last = (c_se - 1) & ~127u;
+            }
+            nt++;
+        }
+        const brb_line::LineDesc d{c_line == kEnd ? brb_line::kOOB : c_line, c_ss, c_se};
+        if (c_line != kEnd)
+            c_line = c_line == c_last ? kEnd : c_line + 128;
+        return d;
+    }
+};
+
 // Line-staged kernel (round 4; line_stream.h).  A wave digests groups of 64 records, one per lane;
 // a lane's VIRTUAL lines are its non-empty segments' 128-byte memory lines in order, staged by
 // LDS-DMA into a three-slot ring: at iteration k the window is lines (k-1, k), line k+1 is in flight
@@ -142,76 +222,18 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
         const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
         brb_md5::FunnelT<RW> f;
         f.init(&fring[wv][0][lane]);
-        // The group's segments are one contiguous range of the arrays (first[] is monotone):
-        // [s0, s1).  They go to this wave's LDS table with coalesced loads, so the stage cursor
-        // below reads them with LDS latency and no vector-memory load ever sits between a wave's
-        // DMA issues (a per-lane load there made hipcc wait for it right before the DMA).  A group
-        // with more segments takes the per-lane path.
-        const uint64_t s0 = brb_digest::uniform64(brb_digest::wave_min64(valid ? k0 : ~uint64_t(0)));
-        const uint64_t s1 = brb_digest::uniform64(brb_digest::wave_max64(valid ? k1 : 0));
-        const uint64_t S = s1 > s0 ? s1 - s0 : 0;
-        if (S > kTab) {
+        SegGroup<kTab> sg{tab_off[wv], tab_len[wv]};
+        if (!sg.plan(soff, slen, k0, k1, valid, dbase, lane)) {   // the per-lane path
             if (valid) {
                 seg_lane(f, data, soff, slen, k0, k1);
                 store_digest(out, rec, f.finish());
             }
             continue;
         }
-        for (uint32_t i = lane; i < uint32_t(S); i += 64) {
-            tab_off[wv][i] = soff[s0 + i];
-            tab_len[wv][i] = slen[s0 + i];
-        }
-        __builtin_amdgcn_s_waitcnt(0);                  // the table is in LDS, every load of it done
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t t0 = uint32_t(k0 - (valid ? s0 : k0)), t1 = uint32_t(k1 - (valid ? s0 : k1));
-        // the group's line span and every lane's stage count (an empty segment costs its lane one
-        // empty stage)
-        uint64_t lo = ~uint64_t(0), hi = 0;
-        uint32_t nl = 0;
-        for (uint32_t t = t0; t < t1; t++) {
-            const uint32_t len = tab_len[wv][t];
-            if (!len) {
-                nl++;
-                continue;
-            }
-            const uint64_t a = dbase + tab_off[wv][t];
-            const uint64_t l0 = a & ~uint64_t(127), l1 = (a + len + 127) & ~uint64_t(127);
-            lo = l0 < lo ? l0 : lo;
-            hi = l1 > hi ? l1 : hi;
-            nl += uint32_t((l1 - l0) >> 7);
-        }
-        lo = brb_digest::uniform64(brb_digest::wave_min64(lo));
-        hi = brb_digest::uniform64(brb_digest::wave_max64(hi));
-        const uint32_t K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
-        if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {   // no line, or too wide
-            if (valid) {
-                seg_lane(f, data, soff, slen, k0, k1);
-                store_digest(out, rec, f.finish());
-            }
-            continue;
-        }
-        const brb_dma::v4i rs = group_rsrc(lo, hi);      // K >= 1 here (some lane has a line)
-
-        // Stage cursor: the line to stage next (offset from lo; kEnd: the cursor must enter the next
-        // segment first) and its segment; nt = the next table entry to enter.
-        constexpr uint32_t kEnd = 0xFFFFFFFFu;
-        uint32_t c_line = kEnd, c_last = 0, c_ss = 0, c_se = 0, nt = t0;
-        auto stage_line = [&]() -> LineDesc {                   // this stage's line; the cursor moves on
-            if (c_line == kEnd && nt < t1) {                    // enter segment nt
-                const uint32_t len = tab_len[wv][nt];
-                if (len) {
-                    c_ss = uint32_t(dbase + tab_off[wv][nt] - lo);
-                    c_se = c_ss + len;
-                    c_line = c_ss & ~127u;
-                    c_last = (c_se - 1) & ~127u;
-                }
-                nt++;
-            }
-            const LineDesc d{c_line == kEnd ? kOOB : c_line, c_ss, c_se};
-            if (c_line != kEnd)
-                c_line = c_line == c_last ? kEnd : c_line + 128;
-            return d;
-        };
+        const uint32_t K = sg.K;
+        const brb_dma::v4i rs = group_rsrc(sg.lo, sg.hi);
+        SegCursor cur{sg.off, sg.len, dbase - sg.lo, sg.t0, sg.t1};
+        auto stage_line = [&]() { return cur.next(); };
         // lines 0 .. NS-1 -> slots 0 .. NS-1; dA, dB (, dC): the lines k-1, k (, k+1) at iteration k
         LineDesc dA = stage_line(), dB = stage_line(), dC = dB;
         issue_rows(rs, lds0, dA.line, lane);
@@ -438,65 +460,19 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
                 store_digest(out, rec, f.finish());
             }
         };
-        const uint64_t s0 = brb_digest::uniform64(brb_digest::wave_min64(valid ? k0 : ~uint64_t(0)));
-        const uint64_t s1 = brb_digest::uniform64(brb_digest::wave_max64(valid ? k1 : 0));
-        const uint64_t S = s1 > s0 ? s1 - s0 : 0;
-        if (S > kTab) {
+        SegGroup<kTab> sg{tab_off[pr], tab_len[pr]};
+        if (!sg.plan(soff, slen, k0, k1, valid, dbase, lane)) {
             alone();
             continue;
         }
-        for (uint32_t i = lane; i < uint32_t(S); i += 64) {
-            tab_off[pr][i] = soff[s0 + i];
-            tab_len[pr][i] = slen[s0 + i];
-        }
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t t0 = uint32_t(k0 - (valid ? s0 : k0)), t1 = uint32_t(k1 - (valid ? s0 : k1));
-        uint64_t lo = ~uint64_t(0), hi = 0;
-        uint32_t nl = 0;
-        for (uint32_t t = t0; t < t1; t++) {
-            const uint32_t len = tab_len[pr][t];
-            if (!len) {
-                nl++;
-                continue;
-            }
-            const uint64_t a = dbase + tab_off[pr][t];
-            const uint64_t l0 = a & ~uint64_t(127), l1 = (a + len + 127) & ~uint64_t(127);
-            lo = l0 < lo ? l0 : lo;
-            hi = l1 > hi ? l1 : hi;
-            nl += uint32_t((l1 - l0) >> 7);
-        }
-        lo = brb_digest::uniform64(brb_digest::wave_min64(lo));
-        hi = brb_digest::uniform64(brb_digest::wave_max64(hi));
-        const uint32_t K = __builtin_amdgcn_readfirstlane(uint32_t(brb_digest::wave_max64(nl)));
-        if (!(hi > lo && hi - lo < (uint64_t(1) << 31) - (uint64_t(1) << 16))) {
-            alone();
-            continue;
-        }
+        const uint32_t K = sg.K;
         wpx[pr][lane] = 0;                              // the consumer reads it only after the plan
         ev[pr][2] = K;                                  // the plan (K >= 1)
         pc_publish(&ev[pr][0], ++pev);
         cexp += 2;
-        const brb_dma::v4i rs = group_rsrc(lo, hi);
-
-        constexpr uint32_t kEnd = 0xFFFFFFFFu;
-        uint32_t c_line = kEnd, c_last = 0, c_ss = 0, c_se = 0, nt = t0;
-        auto stage_line = [&]() -> LineDesc {
-            if (c_line == kEnd && nt < t1) {
-                const uint32_t len = tab_len[pr][nt];
-                if (len) {
-                    c_ss = uint32_t(dbase + tab_off[pr][nt] - lo);
-                    c_se = c_ss + len;
-                    c_line = c_ss & ~127u;
-                    c_last = (c_se - 1) & ~127u;
-                }
-                nt++;
-            }
-            const LineDesc d{c_line == kEnd ? kOOB : c_line, c_ss, c_se};
-            if (c_line != kEnd)
-                c_line = c_line == c_last ? kEnd : c_line + 128;
-            return d;
-        };
+        const brb_dma::v4i rs = group_rsrc(sg.lo, sg.hi);
+        SegCursor cur{sg.off, sg.len, dbase - sg.lo, sg.t0, sg.t1};
+        auto stage_line = [&]() { return cur.next(); };
         LineDesc dA = stage_line(), dB = stage_line();
         issue_rows(rs, lds0, dA.line, lane);
         issue_rows(rs, lds0 + kSlot, dB.line, lane);
