@@ -147,10 +147,11 @@ def test_segments_long_lane_in_wide_group(brb, torch_dev, seg_line):
     t = torch_dev
     far = (1 << 31) + 4099
     big = 96 << 20
-    d = t.empty(far + big + 4096, dtype=t.uint8, device="cuda")
+    size = (far + big + 4096 + 7) // 8 * 8
+    d = t.empty(size, dtype=t.uint8, device="cuda")
     g = t.Generator(device="cuda")
     g.manual_seed(0x10C)
-    d.view(t.int64)[: (far + big + 4096) // 8].random_(generator=g)
+    d.view(t.int64).random_(generator=g)
     n = 128
     first = np.arange(n + 1, dtype=np.uint64) * 2
     offs = (np.arange(2 * n, dtype=np.uint64) * 1000).astype(np.uint64)
