@@ -320,6 +320,148 @@ __global__ __launch_bounds__(kWave) void rc4md5_open_kernel(uint8_t *__restrict_
     g.store(state);
 }
 
+// The RC4 pass as wave pairs (round 4).  rc4_crypt_kernel's lone wave per SIMD spends its issue on
+// the keystream chain (97 us of the 115 us pass with the I/O compiled out, tools/mb/rc4_parts.hip)
+// plus the block loads, their exchange and the sink.  Here the 4 keystream waves of a workgroup
+// each get an I/O wave (wave w + 4): it loads the streams' 64-byte blocks cooperatively
+// (BlockSrcW) into a two-block LDS ring per lane, and stores the results the keystream wave leaves
+// in a second ring; per-lane mailbox counts (staged, taken, produced, stored) order the hand-offs.
+struct Rc4Mail {
+    uint32_t *in_cnt, *in_used, *out_cnt, *out_used;   // this lane's
+};
+
+// false after 2^22 sleeps in which the wave's open lanes saw no progress
+template <class F>
+BRB_DEV bool rc4_wait(F blocked)
+{
+    for (uint32_t spin = 0; spin < (1u << 22); spin++) {
+        if (__builtin_amdgcn_ballot_w64(blocked()) == 0)
+            return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__restrict__ states, const uint8_t *in,
+                                                                   uint8_t *out, const uint64_t *__restrict__ offs,
+                                                                   const uint32_t *__restrict__ lens, uint64_t n,
+                                                                   const uint32_t *__restrict__ sidx,
+                                                                   const uint64_t *__restrict__ ooffs)
+{
+    using brb_line::pc_load;
+    using brb_line::pc_publish;
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    __shared__ uint32_t rin[kWaves][2][16][64];         // staged input blocks, word i of lane l at [.][i][l]
+    __shared__ uint32_t rout[kWaves][2][16][64];        // produced output blocks
+    __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
+    __shared__ uint32_t mb[kWaves][4][64];              // staged, taken, produced, stored (blocks)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w4 = wv % kWaves;
+    for (uint32_t i = threadIdx.x; i < kWaves * 4 * 64; i += 2 * kWave)
+        (&mb[0][0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
+    const bool live = s < n;                           // lanes past n only help with the block loads
+    const uint64_t len = live ? lens[s] : 0;
+    const uint32_t nblk = uint32_t((len + 63) >> 6);
+    const uint32_t nloop = wave_max(nblk);
+    const Rc4Mail m{&mb[w4][0][lane], &mb[w4][1][lane], &mb[w4][2][lane], &mb[w4][3][lane]};
+    if (wv >= kWaves) {
+        // ---- I/O wave
+        const uint64_t off = live ? offs[s] : 0;
+        brb_io::BlockSrcW src;
+        src.init(in + off, len, xch + w4 * kXchBytes);
+        Snk snk;
+        snk.init(out + (live && ooffs ? ooffs[s] : off), len);
+        uint32_t bi = 0, bo = 0;
+        for (uint32_t idle = 0; bo < nloop && idle < (1u << 22);) {
+            // stage block bi once the keystream wave has taken block bi - 2 (its slot is free)
+            if (bi < nloop && __builtin_amdgcn_ballot_w64(bi < nblk && pc_load(m.in_used) + 2 <= bi) == 0) {
+                uint32_t c[16];
+                src.fetch(c);                          // every lane: the loads are cooperative
+                if (bi < nblk) {
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        rin[w4][bi & 1][i][lane] = c[i];
+                    pc_publish(m.in_cnt, bi + 1);
+                }
+                bi++;
+                idle = 0;
+                continue;
+            }
+            // store block bo once produced
+            if (__builtin_amdgcn_ballot_w64(bo < nblk && pc_load(m.out_cnt) < bo + 1) == 0) {
+                if (bo < nblk) {
+                    uint32_t w[16];
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        w[i] = rout[w4][bo & 1][i][lane];
+                    pc_publish(m.out_used, bo + 1);
+                    if (64ull * bo + 64 <= len) {
+                        snk.put16(w);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; i++)
+                            if (64ull * bo + 4 * i < len)
+                                snk.put(w[i]);
+                    }
+                }
+                bo++;
+                idle = 0;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            idle++;
+        }
+        if (live)
+            snk.flush();
+        return;
+    }
+    // ---- keystream wave (issue priority: its chain is the critical path)
+    __builtin_amdgcn_s_setprio(3);
+    Gen g;
+    g.P.lds = slot;
+    g.P.lw = lane * 4 + w4;
+    uint8_t *state = live ? states + uint64_t(sidx ? sidx[s] : s) * kStateBytes : nullptr;
+    if (live)
+        g.load(state);
+    for (uint32_t b = 0; b < nloop; b++) {
+        if (!rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; }))
+            break;                                     // a protocol fault: wrong output, never a hang
+        if (b >= nblk)
+            continue;
+        uint32_t c[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            c[i] = rin[w4][b & 1][i][lane];
+        pc_publish(m.in_used, b + 1);
+        const uint64_t pos = 64ull * b;
+        uint32_t o[16];
+        if (pos + 64 <= len) {
+            uint32_t ks[16];
+            g.words(ks);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                o[i] = c[i] ^ ks[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t q = pos + 4 * i;
+                o[i] = q < len ? c[i] ^ g.next_n(clamp4(len - q)) : 0u;
+            }
+        }
+        if (!rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; }))
+            break;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            rout[w4][b & 1][i][lane] = o[i];
+        pc_publish(m.out_cnt, b + 1);
+    }
+    if (live)
+        g.store(state);
+}
+
 // RC4 + MD5 wave pairs for the read side (round 4).  rc4md5_open_kernel runs one wave per SIMD
 // (65 536 connections = 1 024 waves) whose keystream steps wait on LDS round trips: the SIMD issues
 // in ~59 % of the launch's cycles (roofline.compute.issue_busy_frac of the rc4md5 line), and the
@@ -499,7 +641,9 @@ hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, co
     const int force = brb_opt::get(brb_opt::kRc4Sector);
     if (force >= 0)
         sector_out = force == 1;
-    if (sector_out)
+    if (brb_opt::get(brb_opt::kRc4CryptPair) != 0 && force < 0)
+        rc4_crypt_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
+    else if (sector_out)
         rc4_crypt_kernel<true><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
     else
         rc4_crypt_kernel<false><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);

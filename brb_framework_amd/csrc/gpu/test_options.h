@@ -24,10 +24,11 @@ enum Opt {
                         // at 4, 1 digest_b64_kernel (two LDS slots), 0 the generic DMA kernel
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
     kRc4Pair = 11,      // 1: RC4+MD5 open on RC4 + MD5 wave pairs (default); 0: one wave does both
-    kCount = 12
+    kRc4CryptPair = 12, // 1: the RC4 pass on keystream + I/O wave pairs; 0: one wave per stream does both
+    kCount = 13
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -155,10 +155,17 @@ def _to(torch, a):
 RAGGED = [0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 29, 30, 31, 32, 33, 63, 64, 65, 100, 255, 256, 257, 1000, 1500, 4099]
 
 
+@pytest.fixture(params=[1, 0], ids=["pair", "single"])
+def rc4_pair(request, brb):
+    """Test option rc4_pair: 1 the keystream + I/O wave-pair RC4 pass (default), 0 one wave per stream."""
+    with brb.TestOption("rc4_pair", request.param):
+        yield request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("gaps", [None, 5])
 @pytest.mark.parametrize("base", [0, 1, 2, 3])
-def test_rc4_crypt_batch_ragged(brb, orc, torch_dev, gaps, base):
+def test_rc4_crypt_batch_ragged(brb, orc, torch_dev, gaps, base, rc4_pair):
     lens = (RAGGED * 5)[: 130]
     offs, lens, total = _layout(lens, gaps, base)
     data = workload.gen_records(SEED, base, 1, total + 8)
@@ -182,7 +189,7 @@ def test_rc4_crypt_batch_ragged(brb, orc, torch_dev, gaps, base):
 
 
 @pytest.mark.gpu
-def test_rc4_state_carries_across_calls(brb, orc, torch_dev):
+def test_rc4_state_carries_across_calls(brb, orc, torch_dev, rc4_pair):
     n = 200
     states = brb.rc4_states(_keys(n, 5))
     ts = _to(torch_dev, states)
@@ -199,7 +206,7 @@ def test_rc4_state_carries_across_calls(brb, orc, torch_dev):
 
 
 @pytest.mark.gpu
-def test_rc4_golden_streams(brb, torch_dev, golden):
+def test_rc4_golden_streams(brb, torch_dev, golden, rc4_pair):
     for v in golden["rc4"]["streams"]:
         st = brb.rc4_states([bytes.fromhex(v["key"])])
         data = np.frombuffer(bytes.fromhex(v["data"]), np.uint8).copy()
@@ -425,7 +432,7 @@ def test_rc4_sector_sink_ragged(brb, orc, sector):
 
 
 @pytest.mark.gpu
-def test_rc4_ragged_out_of_place(brb, orc):
+def test_rc4_ragged_out_of_place(brb, orc, rc4_pair):
     """Ragged, packed streams (0..3000 B, the block-edge lengths first) at every input byte offset,
     in place and out of place into an output buffer shifted so that output and input alignments
     differ; device mode, against the oracle, states included; bytes between streams untouched."""
