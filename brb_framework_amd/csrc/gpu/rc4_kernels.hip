@@ -462,66 +462,239 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
         g.store(state);
 }
 
-// RC4 + MD5 wave pairs for the read side (round 4).  rc4md5_open_kernel runs one wave per SIMD
-// (65 536 connections = 1 024 waves) whose keystream steps wait on LDS round trips: the SIMD issues
-// in ~59 % of the launch's cycles (roofline.compute.issue_busy_frac of the rc4md5 line), and the
-// MD5 of the decrypted payload sits on that wave's instruction stream.  rc4md5_open_pair_kernel
-// gives a workgroup the 4 RC4 waves of 256 connections and 4 MD5 waves for the same connections
-// (wave w + 4 beside wave w): the RC4 wave decrypts and drops each MD5 block's 16 message words into
-// a 32-word per-lane LDS ring, posting its count (wpx); the MD5 wave compresses them as they come
-// and posts its own count (cpx).  The RC4 wave writes a block only while the ring has room (block
-// b - 2 compressed) and keeps the SIMD's issue priority: its chain is the critical path.
-// Interleaved rocprofv3 A/B (65 536 x 1 530-byte frames): open 122.9 -> 111.9 us.  The write side
-// measured no gain as a pair (frame 128.1 -> 127.2 us with the payload words passed through the ring,
-// 132.3 us with wave-cooperative loads, 155.9 us with the MD5 wave loading the payload itself): its
-// RC4 wave alone takes as long as the fused kernel, so the frame kernel stays single.
-struct PairRing {
-    uint32_t (*ring)[64];   // [32][64]: word k of lane l at ring[k % 32][l]
-    uint32_t *wpx, *cpx;    // this lane's mailboxes
-    uint32_t lane;
+// RC4 + MD5 frames as wave pairs (round 4).  The fused kernels run one wave per SIMD that does the
+// keystream chain, the MD5 and the I/O.  Here each keystream wave (waves 0..3) gets a partner
+// (wave w + 4) that does everything else: it loads the blocks cooperatively (BlockSrcW) into a
+// two-block LDS ring per lane, computes the MD5, and stores what the keystream wave leaves in a
+// second ring; the mailbox counts of rc4_crypt_pair_kernel order the hand-offs.  The keystream
+// wave keeps the SIMD's issue priority: its chain is the critical path.
+//   frame (write side, ev_kq_aio_transform.c:212-230, 281-283): the partner stages the payload
+//     blocks and digests them; the keystream wave encrypts them (frame chunks 7.., payload shifted
+//     by 2 bytes) and, once the digest is posted, writes the encrypted header;
+//   open (read side + DataValidate, :158-184, 270-279): the partner stages the frame blocks; the
+//     keystream wave decrypts them; the partner stores the plaintext, digests the payload words
+//     (frame bytes 30 + 4w, two plaintext blocks funnel-shifted), checks "HASH:" and the digest and
+//     writes the valid flag.
+// Earlier forms measured (rocprofv3, 65 536 x 1 530-byte frames): fused frame 128.1 us / open
+// 122.9 us; the MD5 alone on the partner with the keystream wave doing the I/O: frame 127.2 us, open
+// 111.1 us.
 
-    // RC4 wave: MD5 block b's words into the ring once block b - 2 is compressed; false on a fault
-    BRB_DEV bool put(uint64_t b, const uint32_t (&m)[16]) const
-    {
-        bool room = false;
-        for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-            if (__builtin_amdgcn_ballot_w64(uint64_t(brb_line::pc_load(cpx)) + 32 < 16 * (b + 1)) == 0) {
-                room = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+// The I/O side of a pair: stage input block bi once block bi - 2 is taken; hand back output block bo
+// once produced.  `stage(c, b)` gets every lane's block b (lanes past their count included: the
+// loads are cooperative); `drain(b)` runs for the lanes whose block b is out.  Returns when every
+// output block is drained (or after 2^22 idle sleeps: a protocol fault, wrong output, no hang).
+template <class Stage, class Drain>
+BRB_DEV void pair_io(const Rc4Mail &m, uint32_t nblk, uint32_t nloop, brb_io::BlockSrcW &src, Stage stage, Drain drain)
+{
+    using brb_line::pc_load;
+    uint32_t bi = 0, bo = 0;
+    for (uint32_t idle = 0; bo < nloop && idle < (1u << 22);) {
+        if (bi < nloop && __builtin_amdgcn_ballot_w64(bi < nblk && pc_load(m.in_used) + 2 <= bi) == 0) {
+            uint32_t c[16];
+            src.fetch(c);
+            stage(c, bi);
+            bi++;
+            idle = 0;
+            continue;
         }
-        const uint32_t q = uint32_t(b & 1) * 16;
+        if (__builtin_amdgcn_ballot_w64(bo < nblk && pc_load(m.out_cnt) < bo + 1) == 0) {
+            if (bo < nblk)
+                drain(bo);
+            bo++;
+            idle = 0;
+            continue;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        idle++;
+    }
+}
+
+__global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *__restrict__ states,
+                                                                      const uint8_t *__restrict__ payload,
+                                                                      const uint64_t *__restrict__ offs,
+                                                                      const uint32_t *__restrict__ lens,
+                                                                      const uint64_t *__restrict__ salts, uint8_t *frames,
+                                                                      const uint64_t *__restrict__ foffs, uint64_t n,
+                                                                      const uint32_t *__restrict__ sidx)
+{
+    using brb_line::pc_load;
+    using brb_line::pc_publish;
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
+    __shared__ uint32_t rin[kWaves][2][16][64];
+    __shared__ uint32_t rout[kWaves][2][16][64];
+    __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
+    __shared__ uint32_t mb[kWaves][4][64];
+    __shared__ uint32_t dg[kWaves][4][64];        // the digests
+    __shared__ uint32_t posted[kWaves];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t w4 = wv % kWaves;
+    for (uint32_t i = threadIdx.x; i < kWaves * 4 * 64; i += 2 * kWave)
+        (&mb[0][0][0])[i] = 0;
+    if (threadIdx.x < kWaves)
+        posted[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
+    const bool live = s < n;
+    const uint64_t len = live ? lens[s] : 0;
+    const uint64_t F = kHeader + len;              // frame bytes
+    const uint32_t nblk = live ? uint32_t(md5_blocks(len)) : 0u;
+    const uint32_t nloop = wave_max(nblk);
+    const Rc4Mail m{&mb[w4][0][lane], &mb[w4][1][lane], &mb[w4][2][lane], &mb[w4][3][lane]};
+    if (wv >= kWaves) {
+        // ---- partner: payload blocks in, MD5 (ev_kq_aio_transform.c:218-222), ciphertext out
+        brb_io::BlockSrcW src;
+        src.init(payload + (live ? offs[s] : 0), len, xch + w4 * kXchBytes);
+        Snk snk;                                  // frame bytes 32..F-1
+        snk.init(live ? frames + foffs[s] + 32 : nullptr, live && F > 32 ? F - 32 : 0);
+        Md5State st = md5_iv();
+        const uint64_t nw = 16 * uint64_t(nblk);
+        pair_io(
+            m, nblk, nloop, src,
+            [&](const uint32_t (&c)[16], uint32_t b) {
+                if (b < nblk) {
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        rin[w4][b & 1][i][lane] = c[i];
+                    pc_publish(m.in_cnt, b + 1);
+                    uint32_t w[16];
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        w[i] = c[i];
+                    md5_pad_block(w, b, len, nw);
+                    md5_compress(st, w);
+                }
+                if (b + 1 == nloop) {             // every block digested: the header can go
+                    dg[w4][0][lane] = st.a;
+                    dg[w4][1][lane] = st.b;
+                    dg[w4][2][lane] = st.c;
+                    dg[w4][3][lane] = st.d;
+                    pc_publish(&posted[w4], 1u);
+                }
+            },
+            [&](uint32_t b) {
+                uint32_t ct[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    ct[i] = rout[w4][b & 1][i][lane];
+                pc_publish(m.out_used, b + 1);
+                if (4 * (16 * uint64_t(b) + 23) <= F) {
+                    if (b == 0) {
+#pragma unroll
+                        for (int i = 1; i < 16; i++)
+                            snk.put(ct[i]);
+                    } else {
+                        snk.put16(ct);
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t i = 0; i < 16; i++) {
+                        const uint64_t w = 16 * uint64_t(b) + i;
+                        if (w != 0 && 4 * (w + 7) < F)
+                            snk.put(ct[i]);
+                    }
+                }
+            });
+        if (nloop == 0)
+            pc_publish(&posted[w4], 1u);
+        if (live)
+            snk.flush();
+        return;
+    }
+    // ---- keystream wave
+    __builtin_amdgcn_s_setprio(3);
+    Gen g;
+    g.P.lds = slot;
+    g.P.lw = lane * 4 + w4;
+    uint8_t *state = live ? states + uint64_t(sidx ? sidx[s] : s) * kStateBytes : nullptr;
+    uint32_t kh[8];                               // keystream of frame chunks 0..7 (the header)
+    if (live) {
+        g.load(state);
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+            kh[k] = g.next4();
+        kh[7] = g.next_n(clamp4(F - 28));
+    }
+    uint32_t prev = 0, first = 0;
+    bool ok = true;
+    for (uint32_t b = 0; b < nloop && ok; b++) {
+        ok = rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; });
+        if (b >= nblk || !ok)
+            continue;
+        uint32_t rw[16], ct[16];
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            ring[q + i][lane] = m[i];
-        brb_line::pc_publish(wpx, uint32_t(16 * (b + 1)));
-        return room;
-    }
-    // MD5 wave: block b's words once posted; false on a fault
-    BRB_DEV bool get(uint64_t b, uint32_t (&m)[16]) const
-    {
-        bool in = false;
-        for (uint32_t spin = 0; spin < (1u << 22); spin++) {
-            if (__builtin_amdgcn_ballot_w64(brb_line::pc_load(wpx) < 16 * (b + 1)) == 0) {
-                in = true;
-                break;
+            rw[i] = rin[w4][b & 1][i][lane];
+        pc_publish(m.in_used, b + 1);
+        if (4 * (16 * uint64_t(b) + 23) <= F) {
+            uint32_t ks[16];
+            if (b == 0) {
+                uint32_t k15[15];
+                g.words(k15);
+#pragma unroll
+                for (int i = 0; i < 15; i++)
+                    ks[i + 1] = k15[i];
+                ks[0] = 0;
+                first = rw[0];
+            } else {
+                g.words(ks);
             }
-            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                ct[i] = __builtin_amdgcn_alignbit(rw[i], prev, 16) ^ ks[i];
+                prev = rw[i];
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 16; i++) {
+                const uint64_t w = 16 * uint64_t(b) + i;
+                const uint32_t raw = rw[i];
+                ct[i] = 0;
+                if (w == 0) {
+                    first = raw;
+                } else {
+                    const uint64_t fb = 4 * (w + 7);   // frame chunk w + 7 = payload bytes 4w - 2 .. 4w + 1
+                    if (fb < F)
+                        ct[i] = __builtin_amdgcn_alignbit(raw, prev, 16) ^ g.next_n(clamp4(F - fb));
+                }
+                prev = raw;
+            }
         }
-        const uint32_t q = uint32_t(b & 1) * 16;
+        ok = rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; });
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            m[i] = ring[q + i][lane];
-        return in;
+            rout[w4][b & 1][i][lane] = ct[i];
+        pc_publish(m.out_cnt, b + 1);
     }
-    BRB_DEV void done(uint64_t b) const { brb_line::pc_publish(cpx, uint32_t(16 * (b + 1))); }
-};
+    if (!live)
+        return;
+    const bool got = brb_line::pc_wait_ge(&posted[w4], 1u) && ok;
+    Md5State st;
+    st.a = dg[w4][0][lane];
+    st.b = dg[w4][1][lane];
+    st.c = dg[w4][2][lane];
+    st.d = dg[w4][3][lane];
+    if (!got)
+        st.a = ~st.a;                             // a protocol fault: a wrong header, never a hang
+    const uint64_t salt = salts[s];
+    uint32_t h[8];
+    h[0] = uint32_t(salt);
+    h[1] = uint32_t(salt >> 32);
+    h[2] = 0x48534148u;                           // "HASH"
+    h[3] = 0x3Au | (st.a << 8);                   // ':' + digest[0..2]
+    h[4] = __builtin_amdgcn_alignbit(st.b, st.a, 24);
+    h[5] = __builtin_amdgcn_alignbit(st.c, st.b, 24);
+    h[6] = __builtin_amdgcn_alignbit(st.d, st.c, 24);
+    h[7] = (st.d >> 24) | (first << 16);          // digest[15], NUL, payload[0], payload[1]
+    Snk hs;
+    hs.init(frames + foffs[s], F < 32 ? F : 32);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        hs.put(h[k] ^ kh[k]);
+    hs.flush();
+    g.store(state);
+}
 
-// The read side as a pair: the RC4 wave decrypts the frame as rc4md5_open_kernel does and drops each
-// MD5 block's 16 payload words (two frame blocks funnel-shifted by 2 bytes) into the ring; the MD5
-// wave compresses them, pads, compares the digest with the decrypted header (posted with block 0)
-// and writes the valid flag.
 __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__restrict__ states, const uint8_t *in,
                                                                      uint8_t *out, const uint64_t *__restrict__ offs,
                                                                      const uint32_t *__restrict__ lens, uint64_t n,
@@ -529,100 +702,134 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
                                                                      const uint32_t *__restrict__ sidx,
                                                                      const uint64_t *__restrict__ ooffs)
 {
+    using brb_line::pc_load;
+    using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
-    __shared__ uint32_t ring[kWaves][32][64];
-    __shared__ uint32_t hdr[kWaves][6][64];       // decrypted header chunks 2..7
-    __shared__ uint32_t wpx[kWaves][64], cpx[kWaves][64];
+    __shared__ uint32_t rin[kWaves][2][16][64];
+    __shared__ uint32_t rout[kWaves][2][16][64];
     __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
+    __shared__ uint32_t mb[kWaves][4][64];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t w4 = wv % kWaves;
-    if (threadIdx.x < kWaves * 64) {
-        (&wpx[0][0])[threadIdx.x] = 0;
-        (&cpx[0][0])[threadIdx.x] = 0;
-    }
+    for (uint32_t i = threadIdx.x; i < kWaves * 4 * 64; i += 2 * kWave)
+        (&mb[0][0][0])[i] = 0;
     __syncthreads();
-    const PairRing pr{ring[w4], &wpx[w4][lane], &cpx[w4][lane], lane};
     const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
+    const bool live = s < n;
+    const uint64_t off = live ? offs[s] : 0, F = live ? lens[s] : 0;
+    const bool framed = live && F >= kHeader;
+    const uint64_t len = framed ? F - kHeader : 0;
+    // frame blocks 0 .. nfb-1: block 0 (the header and payload bytes 0..33), then block b + 1 for
+    // every MD5 block b, as rc4md5_open_kernel
+    const uint32_t nmd = framed ? uint32_t(md5_blocks(len)) : 0u;
+    const uint32_t nfb = live ? 1 + nmd : 0u;
+    const uint32_t nloop = wave_max(nfb);
+    const Rc4Mail m{&mb[w4][0][lane], &mb[w4][1][lane], &mb[w4][2][lane], &mb[w4][3][lane]};
     if (wv >= kWaves) {
-        if (s >= n)
-            return;
-        const uint64_t F = lens[s];
-        // ---- MD5 wave (EvAIOReqTransform_RC4_MD5_DataValidate, ev_kq_aio_transform.c:158-184)
-        uint32_t ok = 0;
-        if (F >= kHeader) {
-            const uint64_t len = F - kHeader;
-            const uint64_t nblk = md5_blocks(len), nw = 16 * nblk;
-            Md5State st = md5_iv();
-            bool in = true;
-            for (uint64_t b = 0; b < nblk && in; b++) {
-                uint32_t m[16];
-                in = pr.get(b, m);
-                md5_pad_block(m, b, len, nw);
-                md5_compress(st, m);
-                pr.done(b);
-            }
-            const uint32_t h2 = hdr[w4][0][lane], h3 = hdr[w4][1][lane], h4 = hdr[w4][2][lane],
-                           h5 = hdr[w4][3][lane], h6 = hdr[w4][4][lane], h7 = hdr[w4][5][lane];
-            const bool tag = h2 == 0x48534148u && (h3 & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
-            const bool dig = __builtin_amdgcn_alignbit(h4, h3, 8) == st.a && __builtin_amdgcn_alignbit(h5, h4, 8) == st.b &&
-                             __builtin_amdgcn_alignbit(h6, h5, 8) == st.c && __builtin_amdgcn_alignbit(h7, h6, 8) == st.d;
-            ok = tag && dig && in;
+        // ---- partner: frame blocks in, plaintext out, MD5 of the payload and the check
+        brb_io::BlockSrcW src;
+        src.init(in + off, F, xch + w4 * kXchBytes);
+        Snk snk;
+        snk.init(live ? out + (ooffs ? ooffs[s] : off) : nullptr, F);
+        Md5State st = md5_iv();
+        const uint64_t nw = 16 * uint64_t(nmd);
+        uint32_t cur[16], h[6] = {0, 0, 0, 0, 0, 0};
+        pair_io(
+            m, nfb, nloop, src,
+            [&](const uint32_t (&c)[16], uint32_t b) {
+                if (b < nfb) {
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        rin[w4][b & 1][i][lane] = c[i];
+                    pc_publish(m.in_cnt, b + 1);
+                }
+            },
+            [&](uint32_t j) {
+                uint32_t pt[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    pt[i] = rout[w4][j & 1][i][lane];
+                pc_publish(m.out_used, j + 1);
+                const uint64_t pos = 64 * uint64_t(j);
+                if (pos + 64 <= F) {
+                    snk.put16(pt);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; i++)
+                        if (pos + 4 * i < F)
+                            snk.put(pt[i]);
+                }
+                if (j == 0) {
+#pragma unroll
+                    for (int q = 0; q < 6; q++)
+                        h[q] = pt[2 + q];
+                } else {                          // MD5 block j - 1: frame blocks j - 1 (cur) and j
+                    uint32_t w[16];
+#pragma unroll
+                    for (int i = 0; i < 16; i++) {
+                        const uint32_t lo = i + 7 < 16 ? cur[i + 7] : pt[i - 9];
+                        const uint32_t hi = i + 8 < 16 ? cur[i + 8] : pt[i - 8];
+                        w[i] = __builtin_amdgcn_alignbit(hi, lo, 16);
+                    }
+                    md5_pad_block(w, j - 1, len, nw);
+                    md5_compress(st, w);
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++)
+                    cur[i] = pt[i];
+            });
+        if (live) {
+            snk.flush();
+            const bool tag = h[0] == 0x48534148u && (h[1] & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
+            const bool dig = __builtin_amdgcn_alignbit(h[2], h[1], 8) == st.a &&
+                             __builtin_amdgcn_alignbit(h[3], h[2], 8) == st.b &&
+                             __builtin_amdgcn_alignbit(h[4], h[3], 8) == st.c &&
+                             __builtin_amdgcn_alignbit(h[5], h[4], 8) == st.d;
+            valid[s] = uint8_t(framed && tag && dig);
         }
-        valid[s] = uint8_t(ok);
         return;
     }
-    // ---- RC4 wave (issue priority: its chain is the critical path; wave-cooperative loads)
+    // ---- keystream wave
     __builtin_amdgcn_s_setprio(3);
-    const bool live = s < n;
     Gen g;
     g.P.lds = slot;
     g.P.lw = lane * 4 + w4;
-    uint8_t *state = nullptr;
-    uint64_t off = 0, F = 0;
-    if (live) {
-        state = states + uint64_t(sidx ? sidx[s] : s) * kStateBytes;
-        g.load(state);
-        off = offs[s];
-        F = lens[s];
-    }
-    brb_io::BlockSrcW src;
-    Snk snk;
-    src.init(in + off, F, xch + w4 * kXchBytes);
-    snk.init(out + (live && ooffs ? ooffs[s] : off), F);
-    uint32_t cur[16], c[16];
-    src.fetch(c);
+    uint8_t *state = live ? states + uint64_t(sidx ? sidx[s] : s) * kStateBytes : nullptr;
     if (live)
-        decrypt_block(c, snk, g, F, 0, cur);
-    const bool framed = live && F >= kHeader;
-    if (framed) {
-#pragma unroll
-        for (int q = 0; q < 6; q++)
-            hdr[w4][q][lane] = cur[2 + q];        // read by the MD5 wave after the first post
-    }
-    const uint64_t nblk = framed ? md5_blocks(F - kHeader) : 0;
-    const uint32_t nloop = wave_max(uint32_t(nblk));
-    for (uint32_t b = 0; b < nloop; b++) {
-        src.fetch(c);
-        if (b >= nblk)
+        g.load(state);
+    bool ok = true;
+    for (uint32_t j = 0; j < nloop && ok; j++) {
+        ok = rc4_wait([&] { return j < nfb && pc_load(m.in_cnt) < j + 1; });
+        if (j >= nfb || !ok)
             continue;
-        uint32_t nxt[16], m[16];
-        decrypt_block(c, snk, g, F, b + 1, nxt);
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const uint32_t lo = i + 7 < 16 ? cur[i + 7] : nxt[i - 9];
-            const uint32_t hi = i + 8 < 16 ? cur[i + 8] : nxt[i - 8];
-            m[i] = __builtin_amdgcn_alignbit(hi, lo, 16);
-        }
-        pr.put(b, m);                             // a fault shows as an invalid frame (the MD5 wave's get)
+        uint32_t c[16], pt[16];
 #pragma unroll
         for (int i = 0; i < 16; i++)
-            cur[i] = nxt[i];
+            c[i] = rin[w4][j & 1][i][lane];
+        pc_publish(m.in_used, j + 1);
+        const uint64_t pos = 64 * uint64_t(j);
+        if (pos + 64 <= F) {
+            uint32_t ks[16];
+            g.words(ks);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                pt[i] = c[i] ^ ks[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t q = pos + 4 * i;
+                pt[i] = q < F ? c[i] ^ g.next_n(clamp4(F - q)) : 0u;
+            }
+        }
+        ok = rc4_wait([&] { return pc_load(m.out_used) + 2 <= j; });
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            rout[w4][j & 1][i][lane] = pt[i];
+        pc_publish(m.out_cnt, j + 1);
     }
-    if (!live)
-        return;
-    snk.flush();
-    g.store(state);
+    if (live)
+        g.store(state);
 }
 
 inline unsigned grid_for(uint64_t n) { return unsigned((n + kWave - 1) / kWave); }
@@ -656,7 +863,11 @@ hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const ui
 {
     if (n == 0)
         return hipSuccess;
-    rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n, sidx);
+    if (brb_opt::get(brb_opt::kRc4Pair) != 0)
+        rc4md5_frame_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n,
+                                                                   sidx);
+    else
+        rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n, sidx);
     return hipGetLastError();
 }
 
