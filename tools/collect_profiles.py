@@ -114,7 +114,7 @@ def main():
     for sub, key, pat, per in (("pmc2", "cfg2_md5", "Md5Alg", 1), ("pmc2s", "cfg2_sha1", "Sha1Alg", 1),
                                ("pmc3", "cfg3_md5", "Md5Alg", 1),
                                ("pmc4", "cfg4_blowfish", "bf_rep_kernel", 1),
-                               ("pmc_rc4", "f1_rc4", "rc4_crypt_kernel", 1),
+                               ("pmc_rc4", "f1_rc4", "rc4_crypt_", 1),
                                ("pmc_rc4md5", "f1_rc4md5", "rc4md5_", 2),
                                ("pmc_md", "f4_metadata", "metadata_", 1),
                                ("pmc_seg", "f4_md5seg", "md5_seg_", 1),
