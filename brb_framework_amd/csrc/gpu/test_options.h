@@ -23,7 +23,7 @@ enum Opt {
     kB64Kernel = 9,     // 64-byte fixed-stride records: 2 digest_b64r_kernel at 8 waves per SIMD (default), 3 the same
                         // at 4, 1 digest_b64_kernel (two LDS slots), 0 the generic DMA kernel
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
-    kRc4Pair = 11,      // 1: RC4+MD5 open on RC4 + MD5 wave pairs (default); 0: one wave does both
+    kRc4Pair = 11,      // 1: RC4+MD5 frame / open on keystream + partner wave pairs (default); 0: one wave
     kRc4CryptPair = 12, // 1: the RC4 pass on keystream + I/O wave pairs; 0: one wave per stream does both
     kCount = 13
 };

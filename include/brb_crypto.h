@@ -392,8 +392,9 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * line-staged producer / consumer wave pairs, the line-staged single waves, the per-lane kernels), "b64_kernel" 2/3/1/0 (64-byte fixed-stride records on
  * the register-buffered kernel at 8 / 4 waves per SIMD, the two-slot kernel, the generic one),
  * "line_slots" 0/2/3 (LDS-DMA ring slots of the line-staged segment and MetaData kernels: each
- * kernel's default, or forced), "rc4md5_pair" 1/0 (BRB_RC4MD5_OpenBatch on RC4 + MD5 wave pairs / one
- * wave per connection).  Returns 1 and the previous
+ * kernel's default, or forced), "rc4md5_pair" 1/0 (BRB_RC4MD5_FrameBatch / OpenBatch on keystream +
+ * partner wave pairs / one wave per connection), "rc4_pair" 1/0 (BRB_RC4_CryptBatch likewise; a forced
+ * "rc4_sector" value selects the one-wave kernel).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

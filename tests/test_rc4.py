@@ -232,8 +232,8 @@ def _oracle_frames(orc, states, payload, offs, lens, salts, frames, foffs):
 
 @pytest.fixture(params=[1, 0], ids=["pair", "single"])
 def rc4md5_pair(request, brb):
-    """Test option rc4md5_pair: 1 the RC4 + MD5 wave-pair open kernel (default), 0 one wave doing both
-    (the frame kernel is the same either way)."""
+    """Test option rc4md5_pair: 1 the keystream + partner wave-pair frame / open kernels (default), 0
+    one wave per connection."""
     with brb.TestOption("rc4md5_pair", request.param):
         yield request.param
 
