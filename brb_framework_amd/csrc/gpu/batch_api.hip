@@ -1016,8 +1016,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"b64_kernel", brb_opt::kB64Kernel, 0, 3},
                  {"line_slots", brb_opt::kLineSlots, 0, 3},
                  {"rc4md5_pair", brb_opt::kRc4Pair, 0, 1},
-                 {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1},
-                 {"line_pair", brb_opt::kLinePair, 0, 1}};
+                 {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

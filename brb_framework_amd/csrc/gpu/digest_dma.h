@@ -11,7 +11,6 @@
 #pragma once
 
 #include "digest_line.h"
-#include "digest_line_pair.h"
 #include "digest_var_line.h"
 #include "dma_stage.h"
 

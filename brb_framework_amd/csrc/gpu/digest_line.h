@@ -329,4 +329,23 @@ inline unsigned device_cu_count()
     return n;
 }
 
+// One 8-wave workgroup per CU (128 KiB of LDS), persistent, groups handed out by tickets (DYN), DMA
+// with the non-temporal policy (every line is read exactly once).  Measured with
+// tools/mb/md5_ab.hip, MD5, medians of 20-launch bursts:
+//   1 Mi x 1500 B: 316 us static 4-wave workgroups -> 300 us (read floor of the same bytes: 261 us nt)
+//   cfg2 65 536 x 1500 B: 25.3 us (record-relative 128-byte stages) -> 24.9 us
+template <class Alg>
+hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
+                             hipStream_t s)
+{
+    constexpr int W = 8;
+    const uint64_t groups = (n_rec + 63) / 64;
+    const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
+    if (out_al)
+        digest_line_kernel<Alg, W, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    else
+        digest_line_kernel<Alg, W, false, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    return hipGetLastError();
+}
+
 }  // namespace brb_digest

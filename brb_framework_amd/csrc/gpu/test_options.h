@@ -25,11 +25,10 @@ enum Opt {
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
     kRc4Pair = 11,      // 1: RC4+MD5 frame / open on keystream + partner wave pairs (default); 0: one wave
     kRc4CryptPair = 12, // 1: the RC4 pass on keystream + I/O wave pairs; 0: one wave per stream does both
-    kLinePair = 13,     // 1: fixed-stride digests with one group per SIMD on stager + hasher wave pairs
-    kCount = 14
+    kCount = 13
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -140,33 +140,6 @@ def test_large_batch_staging(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
-@pytest.mark.parametrize("pair", [1, 0])
-@pytest.mark.parametrize("n,rec_len,off", [
-    (65536, 1500, 0),        # cfg2's shape: one group per SIMD
-    (65500, 1500, 4),        # partial last group, record bases 4 mod 16
-    (40000, 1532, 8),        # t = 60: two padding blocks
-    (30001, 1536, 12),       # t = 0: the padding block is a constant
-    (9000, 68, 0),           # K = 1: two lines, one window
-    (9000, 128, 4),          # K = 1, t = 0
-    (7777, 196, 8),          # K = 2, t = 4
-    (64, 4096, 0),           # one group, 32 windows
-    (1, 1500, 4),            # one record
-])
-def test_fixed_line_pairs(brb, orc, torch_dev, pair, n, rec_len, off):
-    """Fixed-stride 4-byte-aligned records with at most one group per SIMD: the stager + hasher
-    wave pairs (test option line_pair 1, digest_line_pair.h) and the single-wave line kernel (0),
-    MD5 and SHA-1, every record vs the oracle."""
-    data = workload.gen_records(0x5EED0011, 0, n, rec_len)
-    d = torch_dev.zeros(data.size + 64, dtype=torch_dev.uint8, device="cuda")
-    d[off:off + data.size] = to_dev(torch_dev, data)
-    view = d[off:off + data.size]
-    with brb.TestOption("line_pair", pair):
-        got5 = brb.md5_batch_fixed(view, rec_len, n).cpu().numpy()
-        got1 = brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy()
-    assert np.array_equal(got5, orc.md5_batch_fixed(data, rec_len, n, threads=16))
-    assert np.array_equal(got1, orc.sha1_batch_fixed(data, rec_len, n, threads=16))
-
-
 @pytest.mark.parametrize("kernel", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,off", [(1, 0), (64, 4), (65, 8), (4096 * 64 + 7, 0), (1 << 20, 12), (2048 * 4 * 64 * 3 + 65, 4)])
 def test_b64_kernels_exact_buffer(brb, orc, torch_dev, kernel, n, off):
