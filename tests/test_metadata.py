@@ -197,6 +197,37 @@ def test_unpack_batch_bench_count(brb, orc, seg_line):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seg_line", [1, 2])
+def test_unpack_many_groups_per_wave(brb, orc, seg_line):
+    """More groups than the launch has waves (line kernel) or wave pairs (pair kernel): 200 000
+    packs = 3 125 groups on at most 1 024, three or four groups in sequence per wave / pair.  The
+    packs are 3 000 corpus packs repeated at scattered offsets; the whole buffer is copied a second
+    time past 2 GiB, and one pack of every fifth group is read from that copy, so those groups take
+    the per-lane path (the producer alone) between planned ones.  Every field vs the oracle."""
+    import torch
+    uniq = corpus(29, 3000)
+    want_u = [orc.metadata_unpack(p) for p in uniq]
+    n = 200_000
+    idx = np.random.default_rng(30).integers(0, len(uniq), n)
+    buf, offs, lens = scatter(np.random.default_rng(31), [uniq[i] for i in idx])
+    far = (1 << 31) + 777
+    d = torch.zeros(far + buf.size, dtype=torch.uint8, device="cuda")
+    src = torch.from_numpy(buf).cuda()
+    d[: buf.size] = src
+    d[far:] = src
+    groups = (n + 63) // 64
+    wide = [64 * g + 9 for g in range(2, groups, 5)]
+    offs[wide] += np.uint64(far)
+    o = torch.from_numpy(offs.view(np.int64)).cuda()
+    ln = torch.from_numpy(lens.view(np.int32)).cuda()
+    with brb.TestOption("seg_line", seg_line):
+        dev = brb.metadata_unpack_batch(d, o, ln).cpu().numpy().reshape(-1).view(brb.METADATA_INFO_DTYPE)
+    assert infos_as_tuples(dev) == [want_u[i] for i in idx]
+    del d, src
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_line", [1, 2])
 @pytest.mark.parametrize("n_items,item_len,gap", [(4, 375, 0), (9, 61, 3), (40, 2, 1), (2, 1000, 77), (13, 0, 5)])
 def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap, seg_line):
     """Batches whose packs share one layout (the bench's 4 x 375-byte items, and tiny / empty /

@@ -137,6 +137,51 @@ def test_segments_mixed_wide_groups(brb, torch_dev, seg_line):
     t.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_many_groups_per_wave(brb, torch_dev, seg_line):
+    """More groups than the launch has waves (line kernel) or wave pairs (pair kernel): 200 000
+    records = 3 125 groups on at most 1 024, so each wave / pair runs three or four groups in
+    sequence and the pair protocol's events carry over from group to group.  Every seventh group is
+    wide (one segment past 2 GiB: the per-lane path, in the pair kernel the producer alone), so one
+    pair's sequence mixes planned groups and groups it runs alone.  Every record against the
+    per-lane kernel, a sample (all wide groups among it) against hashlib."""
+    t = torch_dev
+    far = (1 << 31) + 4099
+    size = far + (1 << 20)
+    d = t.empty(size, dtype=t.uint8, device="cuda")
+    lo_h = workload.gen_records(0x5EED00F9, 0, 1, 1 << 20)
+    hi_h = workload.gen_records(0x5EED00FA, 0, 1, 1 << 20)
+    d[: lo_h.size] = t.from_numpy(lo_h).cuda()
+    d[far:far + hi_h.size] = t.from_numpy(hi_h).cuda()
+    rng = np.random.default_rng(43)
+    n = 200_000
+    groups = (n + 63) // 64
+    wide_rec = [64 * g + 11 for g in range(3, groups, 7)]
+    counts = rng.integers(0, 4, n)
+    counts[wide_rec] = np.maximum(counts[wide_rec], 1)
+    first = np.zeros(n + 1, np.uint64)
+    first[1:] = np.cumsum(counts)
+    nseg = int(first[-1])
+    lens = rng.integers(0, 400, nseg).astype(np.uint32)
+    offs = rng.integers(0, (1 << 20) - 500, nseg).astype(np.uint64)
+    offs[first[wide_rec].astype(np.int64)] += np.uint64(far)
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    o, ln, fi = dev(offs), dev(lens), dev(first)
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
+    with brb.TestOption("seg_line", 0):
+        ref = brb.md5_batch_segments(d, o, ln, fi).cpu().numpy()
+    assert np.array_equal(got, ref)
+    for i in sorted(set(wide_rec) | set(range(0, n, 211)) | {n - 1}):
+        parts = []
+        for k in range(int(first[i]), int(first[i + 1])):
+            a, m = int(offs[k]), int(lens[k])
+            parts.append((hi_h[a - far:a - far + m] if a >= far else lo_h[a:a + m]).tobytes())
+        assert got[i].tobytes() == hashlib.md5(b"".join(parts)).digest(), i
+    del d
+    t.cuda.empty_cache()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seg_line", [1, 2])
 def test_segments_long_lane_in_wide_group(brb, torch_dev, seg_line):
