@@ -19,6 +19,7 @@ BATCH_ASYNC = 0x2
 BATCH_ALL_DEVICES = 0x4
 BATCH_DROPPED = -2
 BATCH_PARTIAL = -3
+BATCH_FAULT = -4
 TRANSFORM_DROPPED = -1
 
 u8p = ctypes.POINTER(ctypes.c_uint8)

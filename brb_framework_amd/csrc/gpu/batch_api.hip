@@ -103,6 +103,7 @@ namespace brb_api {
 // (an event thread that ends returns its HBM) or by BRB_CryptoGPU_ThreadCleanup().
 struct Workspaces {
     std::vector<std::pair<void *, size_t>> by_dev;   // (ptr, capacity) per device ordinal
+    std::vector<uint32_t *> fault_by_dev;             // pair_fault.h: the thread's fault word per device
     void release()
     {
         for (size_t d = 0; d < by_dev.size(); d++)
@@ -111,10 +112,66 @@ struct Workspaces {
                 (void)hipFree(by_dev[d].first);
                 by_dev[d] = {nullptr, 0};
             }
+        for (uint32_t *&w : fault_by_dev)
+            if (w) {
+                (void)hipHostFree(w);
+                w = nullptr;
+            }
     }
     ~Workspaces() { release(); }
 };
 thread_local Workspaces t_ws;
+thread_local uint32_t *t_fault_armed = nullptr;       // the word the pair kernels' launchers pass
+
+// The calling thread's fault word on the current device: page-locked, device-mapped, coherent host
+// memory (the kernel's store is visible once the stream has drained).  nullptr if it cannot be had.
+uint32_t *fault_word()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (t_ws.fault_by_dev.size() <= size_t(dev))
+        t_ws.fault_by_dev.resize(dev + 1, nullptr);
+    uint32_t *&w = t_ws.fault_by_dev[dev];
+    if (!w) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        w = static_cast<uint32_t *>(p);
+    }
+    return w;
+}
+
+// Arms the thread's fault word for one synchronous call (pair_fault.h); check() after the stream
+// has drained turns a fault into BRB_BATCH_FAULT.  Unarmed for device-mode async calls.
+struct PairFault {
+    uint32_t *w = nullptr;
+    explicit PairFault(unsigned flags)
+    {
+        if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC))
+            return;
+        w = fault_word();
+        if (w) {
+            __atomic_store_n(w, 0u, __ATOMIC_RELAXED);
+            t_fault_armed = w;
+        }
+    }
+    ~PairFault() { t_fault_armed = nullptr; }
+    PairFault(const PairFault &) = delete;
+    PairFault &operator=(const PairFault &) = delete;
+    int check(int rc) const
+    {
+        if (rc != BRB_BATCH_OK || !w || __atomic_load_n(w, __ATOMIC_ACQUIRE) == 0)
+            return rc;
+        set_err("wave-pair protocol fault: a kernel's bounded wait on its partner wave gave up; the "
+                "outputs (and RC4 states) of this call are wrong");
+        return BRB_BATCH_FAULT;
+    }
+};
 
 void release_thread_resources()
 {
@@ -152,8 +209,16 @@ void *workspace(size_t bytes, hipError_t *err)
 
 }  // namespace brb_api
 
+namespace brb {
+uint32_t *pair_fault_word()
+{
+    return brb_api::t_fault_armed;
+}
+}  // namespace brb
+
 namespace {
 
+using brb_api::PairFault;
 using brb_api::workspace;
 
 inline size_t align_up(size_t x, size_t a)
@@ -447,13 +512,14 @@ int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint
             });
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const PairFault pf(flags);                       // pair_fault.h
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
         e = brb::launch_rc4_crypt(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(in),
                                   static_cast<uint8_t *>(out), offsets, lengths, n, s);
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
-        return finish(s, flags);
+        return pf.check(finish(s, flags));
     }
     uint64_t lo, hi;
     if (!span_of(offsets, lengths, n, 0, lo, hi))
@@ -473,7 +539,7 @@ int rc4_crypt_batch(BRB_RC4_State *states, const void *in, void *out, const uint
                                    reinterpret_cast<const uint32_t *>(st.dev(i_len)), n, s)) != hipSuccess)
         rc = fail_hip("kernel launch", e);
     if (rc == BRB_BATCH_OK)
-        return st.download(s);
+        return pf.check(st.download(s));
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -502,13 +568,14 @@ int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_
             });
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const PairFault pf(flags);                       // pair_fault.h
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
         e = brb::launch_rc4md5_frame(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(payload), offsets,
                                      lengths, salts, static_cast<uint8_t *>(frames), frame_offsets, n, s);
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
-        return finish(s, flags);
+        return pf.check(finish(s, flags));
     }
     uint64_t plo, phi, flo, fhi;
     if (!span_of(offsets, lengths, n, 0, plo, phi) || !span_of(frame_offsets, lengths, n, BRB_RC4MD5_HEADER, flo, fhi))
@@ -530,7 +597,7 @@ int rc4md5_frame_batch(BRB_RC4_State *states, const void *payload, const uint64_
                                       reinterpret_cast<const uint64_t *>(st.dev(i_fo)), n, s)) != hipSuccess)
         rc = fail_hip("kernel launch", e);
     if (rc == BRB_BATCH_OK)
-        return st.download(s);
+        return pf.check(st.download(s));
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -558,13 +625,14 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
             });
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const PairFault pf(flags);                       // pair_fault.h
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
         e = brb::launch_rc4md5_open(reinterpret_cast<uint8_t *>(states), static_cast<const uint8_t *>(frames),
                                     static_cast<uint8_t *>(out), offsets, lengths, n, valid, s);
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
-        return finish(s, flags);
+        return pf.check(finish(s, flags));
     }
     uint64_t lo, hi;
     if (!span_of(offsets, lengths, n, 0, lo, hi))
@@ -584,7 +652,7 @@ int rc4md5_open_batch(BRB_RC4_State *states, const void *frames, void *out, cons
                                      reinterpret_cast<const uint32_t *>(st.dev(i_len)), n, st.dev(i_val), s)) != hipSuccess)
         rc = fail_hip("kernel launch", e);
     if (rc == BRB_BATCH_OK)
-        return st.download(s);
+        return pf.check(st.download(s));
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -609,13 +677,14 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
                                 flags & ~BRB_BATCH_ALL_DEVICES, nullptr);
         });
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const PairFault pf(flags);                       // pair_fault.h
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
         e = brb::launch_md5_segments(static_cast<const uint8_t *>(data), soff, slen, first, n_rec,
                                      static_cast<uint8_t *>(digests), s);
         if (e != hipSuccess)
             return fail_hip("kernel launch", e);
-        return finish(s, flags);
+        return pf.check(finish(s, flags));
     }
     // host mode: rebase the segment lists to start at 0 and copy the byte span they cover
     const uint64_t k0 = first[0], nseg = first[n_rec] - k0;
@@ -644,7 +713,7 @@ int md5_segments(const void *data, const uint64_t *soff, const uint32_t *slen, c
                                       reinterpret_cast<const uint64_t *>(st.dev(i_f)), n_rec, st.dev(i_out), s)) != hipSuccess)
         rc = fail_hip("kernel launch", e);
     if (rc == BRB_BATCH_OK)
-        return st.download(s);
+        return pf.check(st.download(s));
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -669,11 +738,12 @@ int metadata_unpack(const void *data, const uint64_t *offs, const uint32_t *lens
             return metadata_unpack(data, offs + lo, lens + lo, hi - lo, info + lo, flags & ~BRB_BATCH_ALL_DEVICES, nullptr);
         });
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const PairFault pf(flags);                       // pair_fault.h
     hipError_t e;
     if (flags & BRB_BATCH_DEVICE) {
         if ((e = brb::launch_metadata_unpack(static_cast<const uint8_t *>(data), offs, lens, n, info, s)) != hipSuccess)
             return fail_hip("kernel launch", e);
-        return finish(s, flags);
+        return pf.check(finish(s, flags));
     }
     // host mode: copy the byte span the packs cover, with the offsets rebased to it
     uint64_t lo, hi;
@@ -692,7 +762,7 @@ int metadata_unpack(const void *data, const uint64_t *offs, const uint32_t *lens
                                          reinterpret_cast<BRB_MetaDataUnpackInfo *>(st.dev(i_out)), s)) != hipSuccess)
         rc = fail_hip("kernel launch", e);
     if (rc == BRB_BATCH_OK)
-        return st.download(s);
+        return pf.check(st.download(s));
     (void)hipStreamSynchronize(s);
     return rc;
 }
@@ -1016,7 +1086,8 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"b64_kernel", brb_opt::kB64Kernel, 0, 3},
                  {"line_slots", brb_opt::kLineSlots, 0, 3},
                  {"rc4md5_pair", brb_opt::kRc4Pair, 0, 1},
-                 {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1}};
+                 {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1},
+                 {"pair_stall", brb_opt::kPairStall, 0, 1}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -6,6 +6,7 @@
 
 #include "brb_crypto.h"
 #include "brb_gpu_common.h"
+#include "pair_fault.h"
 
 namespace brb {
 

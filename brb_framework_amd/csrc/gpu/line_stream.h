@@ -343,7 +343,7 @@ BRB_DEV bool emit_line(brb_md5::FunnelT<RW> &f, Emit &e, const uint32_t (&dw)[36
 // Consumer: compresses the lane's words as the producer posts them (wpx), posting its own count
 // (cpx), until the producer's event count reaches `end` (its last post is in by then).  False when
 // the producer stopped (2^22 sleeps with no word, no end and no beat of hb: a protocol fault; the
-// launch's digests are then wrong, but it ends).
+// launch's digests are then wrong, but it ends, and the caller reports it: pair_fault.h).
 template <uint32_t RW>
 BRB_DEV bool pc_consume(brb_md5::FunnelT<RW> &f, uint32_t *ev_p, uint32_t end, uint32_t *wpx, uint32_t *cpx,
                         uint32_t *hb, uint64_t *idle = nullptr)

@@ -359,7 +359,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
                                                              const uint64_t *__restrict__ soff,
                                                              const uint32_t *__restrict__ slen,
                                                              const uint64_t *__restrict__ first, uint64_t n_rec,
-                                                             uint8_t *__restrict__ out)
+                                                             uint8_t *__restrict__ out, uint32_t *fault, uint32_t stall)
 {
     using namespace brb_line;
     constexpr uint32_t RW = 64;                         // funnel ring words per lane (16 KiB per pair)
@@ -393,8 +393,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         const uint64_t c_t0 = __builtin_amdgcn_s_memtime();
 #endif
         for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
-            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3]))
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3])) {
+                pc_fault(fault);
                 return;
+            }
             pseen++;
             const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
             pc_publish(&ev[pr][1], ++cev);              // plan read
@@ -403,11 +405,15 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
 #ifdef BRB_LINE_STAMPS
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3], &c_wait))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3], &c_wait)) {
+                pc_fault(fault);
                 return;
+            }
 #else
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3]))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3])) {
+                pc_fault(fault);
                 return;
+            }
 #endif
             pseen++;
             const uint32_t a = fin[pr][0][lane];
@@ -444,8 +450,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     const uint64_t p_t0 = __builtin_amdgcn_s_memtime();
 #endif
     for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
-        if (!pc_wait_ge(&ev[pr][1], cexp))             // every earlier event acknowledged
+        if (!pc_wait_ge(&ev[pr][1], cexp)) {           // every earlier event acknowledged
+            pc_fault(fault);
             return;
+        }
         const uint64_t rec = g * 64 + lane;
         const bool valid = rec < n_rec;
         const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
@@ -468,7 +476,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         const uint32_t K = sg.K;
         wpx[pr][lane] = 0;                              // the consumer reads it only after the plan
         ev[pr][2] = K;                                  // the plan (K >= 1)
-        pc_publish(&ev[pr][0], ++pev);
+        if (stall && blockIdx.x == 0 && pr == 0 && pev == 0)
+            ++pev;                                      // test option pair_stall: the plan is never posted
+        else
+            pc_publish(&ev[pr][0], ++pev);
         cexp += 2;
         const brb_dma::v4i rs = group_rsrc(sg.lo, sg.hi);
         SegCursor cur{sg.off, sg.len, dbase - sg.lo, sg.t0, sg.t1};
@@ -525,8 +536,10 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                       // the stray stage past K, before the slots are reused
-        if (!ok)
+        if (!ok) {
+            pc_fault(fault);
             return;
+        }
         fin[pr][0][lane] = uint32_t(f.acc) | (f.nacc << 24);
         fin[pr][1][lane] = uint32_t(f.total);
         fin[pr][2][lane] = uint32_t(f.total >> 32);
@@ -558,7 +571,8 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
         constexpr int NP = 4;                          // 4 pairs, 159 KiB of LDS: one workgroup per CU
         const uint64_t wgs = (groups + NP - 1) / NP;
         const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-        md5_seg_pc_kernel<NP><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out);
+        md5_seg_pc_kernel<NP><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out, brb::pair_fault_word(),
+                                                        uint32_t(brb_opt::get(brb_opt::kPairStall)));
         return hipGetLastError();
     }
     constexpr int W = 4;                               // 4 x (8 NS + 14) KiB of LDS: one workgroup per CU

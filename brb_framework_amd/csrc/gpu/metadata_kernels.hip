@@ -194,7 +194,8 @@ template <int W, int NS, bool PC>
 __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(const uint8_t *__restrict__ data,
                                                                                const uint64_t *__restrict__ offs,
                                                                                const uint32_t *__restrict__ lens, uint64_t n,
-                                                                               BRB_MetaDataUnpackInfo *__restrict__ info)
+                                                                               BRB_MetaDataUnpackInfo *__restrict__ info,
+                                                                               uint32_t *fault, uint32_t stall)
 {
     using namespace brb_line;
     constexpr uint32_t RW = PC ? 64 : brb_line::kRingWords;
@@ -225,8 +226,10 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
         // ---------------- consumer ----------------
         uint32_t pseen = 0, cev = 0;
         for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
-            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3]))
+            if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3])) {
+                pc_fault(fault);
                 return;
+            }
             pseen++;
             const uint32_t K = __builtin_amdgcn_readfirstlane(ev[pr][2]);
             pc_publish(&ev[pr][1], ++cev);              // plan read
@@ -234,8 +237,10 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
                 continue;                               // the producer runs this group alone
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
-            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3]))
+            if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3])) {
+                pc_fault(fault);
                 return;
+            }
             pseen++;
             uint32_t v[15];
 #pragma unroll
@@ -276,8 +281,10 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
     uint32_t beats = 0;                                 // pairs: heartbeat, one per line
 
     for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
-        if (PC && !pc_wait_ge(&ev[pr][1], cexp))        // every earlier event acknowledged
+        if (PC && !pc_wait_ge(&ev[pr][1], cexp)) {      // every earlier event acknowledged
+            pc_fault(fault);
             return;
+        }
         const uint64_t r = g * 64 + lane;
         const bool valid = r < n;
         const uint64_t base = valid ? dbase + offs[r] : dbase;
@@ -308,7 +315,10 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
         if (PC) {
             *my_wpx = 0;                                  // the consumer reads it only after the plan
             ev[pr][2] = K;
-            pc_publish(&ev[pr][0], ++pev);
+            if (stall && blockIdx.x == 0 && pr == 0 && pev == 0)
+                ++pev;                                    // test option pair_stall: the plan is never posted
+            else
+                pc_publish(&ev[pr][0], ++pev);
             cexp += 2;
         }
         const brb_dma::v4i rs = group_rsrc(lo, hi);
@@ -454,8 +464,10 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
             }
         }
         brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
-        if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)
-            return;                                              // a protocol fault (wrong results, no hang)
+        if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0) {
+            pc_fault(fault);                                     // a protocol fault: reported, no hang
+            return;
+        }
         if (phase != kDone) {                                    // a pack shorter than its header
             uint32_t dw[36] = {};
             events(int64_t(1) << 62, int64_t(1) << 62, 0, 0, dw, true);
@@ -506,13 +518,14 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
     if (brb_opt::get(brb_opt::kSegLine) == 2)          // wave pairs
-        metadata_line_kernel<W, 2, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info);
+        metadata_line_kernel<W, 2, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info, brb::pair_fault_word(),
+                                                                  uint32_t(brb_opt::get(brb_opt::kPairStall)));
     // three slots by default: 43.6 vs 49.3 us with two (bench --op metadata, interleaved A/B,
     // gpurun_out/r04s_md); test option line_slots 2 for the other
     else if (brb_opt::get(brb_opt::kLineSlots) == 2)
-        metadata_line_kernel<W, 2, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+        metadata_line_kernel<W, 2, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr, 0u);
     else
-        metadata_line_kernel<W, 3, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info);
+        metadata_line_kernel<W, 3, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr, 0u);
     return hipGetLastError();
 }
 

@@ -3,7 +3,8 @@
 // One writer per counter or mailbox: release store after the data it covers, acquire load before
 // the reads it guards (workgroup scope: both waves are in one workgroup, so LDS and the CU's L1 are
 // shared).  Every wait is bounded (~2^22 sleeps without progress from the other wave): a protocol
-// fault gives wrong results, never a hung wave.
+// fault never hangs a wave; its outputs are wrong, and the wave that gives up stores 1 into the
+// call's fault word (pc_fault; pair_fault.h), so the batch call fails instead of returning them.
 #pragma once
 
 #include "brb_gpu_common.h"
@@ -62,5 +63,13 @@ BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
     __hip_atomic_store(ctr, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// A bounded wait gave up: flag the call (a word of page-locked host memory, pair_fault.h; nullptr
+// when the call is not armed).  A vector store at system scope, read by the host after the launch
+// has completed.
+BRB_DEV void pc_fault(uint32_t *fault)
+{
+    if (fault)
+        __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 }  // namespace brb_line

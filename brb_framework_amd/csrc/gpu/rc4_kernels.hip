@@ -346,8 +346,10 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
                                                                    uint8_t *out, const uint64_t *__restrict__ offs,
                                                                    const uint32_t *__restrict__ lens, uint64_t n,
                                                                    const uint32_t *__restrict__ sidx,
-                                                                   const uint64_t *__restrict__ ooffs)
+                                                                   const uint64_t *__restrict__ ooffs, uint32_t *fault,
+                                                                   uint32_t stall)
 {
+    using brb_line::pc_fault;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -374,13 +376,15 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
         src.init(in + off, len, xch + w4 * kXchBytes);
         Snk snk;
         snk.init(out + (live && ooffs ? ooffs[s] : off), len);
+        // test option pair_stall: the first workgroup's first I/O wave never hands a block over
+        const bool stalled = stall && blockIdx.x == 0 && w4 == 0;
         uint32_t bi = 0, bo = 0;
         for (uint32_t idle = 0; bo < nloop && idle < (1u << 22);) {
             // stage block bi once the keystream wave has taken block bi - 2 (its slot is free)
             if (bi < nloop && __builtin_amdgcn_ballot_w64(bi < nblk && pc_load(m.in_used) + 2 <= bi) == 0) {
                 uint32_t c[16];
                 src.fetch(c);                          // every lane: the loads are cooperative
-                if (bi < nblk) {
+                if (bi < nblk && !stalled) {
 #pragma unroll
                     for (int i = 0; i < 16; i++)
                         rin[w4][bi & 1][i][lane] = c[i];
@@ -414,6 +418,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
             __builtin_amdgcn_s_sleep(1);
             idle++;
         }
+        if (bo < nloop)
+            pc_fault(fault);                           // a protocol fault: reported, never a hang
         if (live)
             snk.flush();
         return;
@@ -427,8 +433,10 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
     if (live)
         g.load(state);
     for (uint32_t b = 0; b < nloop; b++) {
-        if (!rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; }))
-            break;                                     // a protocol fault: wrong output, never a hang
+        if (!rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; })) {
+            pc_fault(fault);                           // a protocol fault: reported, never a hang
+            break;
+        }
         if (b >= nblk)
             continue;
         uint32_t c[16];
@@ -451,8 +459,10 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
                 o[i] = q < len ? c[i] ^ g.next_n(clamp4(len - q)) : 0u;
             }
         }
-        if (!rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; }))
+        if (!rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; })) {
+            pc_fault(fault);
             break;
+        }
 #pragma unroll
         for (int i = 0; i < 16; i++)
             rout[w4][b & 1][i][lane] = o[i];
@@ -482,9 +492,9 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
 // The I/O side of a pair: stage input block bi once block bi - 2 is taken; hand back output block bo
 // once produced.  `stage(c, b)` gets every lane's block b (lanes past their count included: the
 // loads are cooperative); `drain(b)` runs for the lanes whose block b is out.  Returns when every
-// output block is drained (or after 2^22 idle sleeps: a protocol fault, wrong output, no hang).
+// output block is drained (true), or after 2^22 idle sleeps (false: a protocol fault, no hang).
 template <class Stage, class Drain>
-BRB_DEV void pair_io(const Rc4Mail &m, uint32_t nblk, uint32_t nloop, brb_io::BlockSrcW &src, Stage stage, Drain drain)
+BRB_DEV bool pair_io(const Rc4Mail &m, uint32_t nblk, uint32_t nloop, brb_io::BlockSrcW &src, Stage stage, Drain drain)
 {
     using brb_line::pc_load;
     uint32_t bi = 0, bo = 0;
@@ -507,6 +517,7 @@ BRB_DEV void pair_io(const Rc4Mail &m, uint32_t nblk, uint32_t nloop, brb_io::Bl
         __builtin_amdgcn_s_sleep(1);
         idle++;
     }
+    return bo >= nloop;
 }
 
 __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *__restrict__ states,
@@ -515,8 +526,9 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
                                                                       const uint32_t *__restrict__ lens,
                                                                       const uint64_t *__restrict__ salts, uint8_t *frames,
                                                                       const uint64_t *__restrict__ foffs, uint64_t n,
-                                                                      const uint32_t *__restrict__ sidx)
+                                                                      const uint32_t *__restrict__ sidx, uint32_t *fault)
 {
+    using brb_line::pc_fault;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -549,7 +561,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
         snk.init(live ? frames + foffs[s] + 32 : nullptr, live && F > 32 ? F - 32 : 0);
         Md5State st = md5_iv();
         const uint64_t nw = 16 * uint64_t(nblk);
-        pair_io(
+        const bool io_ok = pair_io(
             m, nblk, nloop, src,
             [&](const uint32_t (&c)[16], uint32_t b) {
                 if (b < nblk) {
@@ -595,6 +607,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
                     }
                 }
             });
+        if (!io_ok)
+            pc_fault(fault);
         if (nloop == 0)
             pc_publish(&posted[w4], 1u);
         if (live)
@@ -666,6 +680,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
             rout[w4][b & 1][i][lane] = ct[i];
         pc_publish(m.out_cnt, b + 1);
     }
+    if (!ok)
+        pc_fault(fault);
     if (!live)
         return;
     const bool got = brb_line::pc_wait_ge(&posted[w4], 1u) && ok;
@@ -674,8 +690,10 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
     st.b = dg[w4][1][lane];
     st.c = dg[w4][2][lane];
     st.d = dg[w4][3][lane];
-    if (!got)
-        st.a = ~st.a;                             // a protocol fault: a wrong header, never a hang
+    if (!got) {
+        st.a = ~st.a;                             // a protocol fault: a wrong header, reported, never a hang
+        pc_fault(fault);
+    }
     const uint64_t salt = salts[s];
     uint32_t h[8];
     h[0] = uint32_t(salt);
@@ -700,8 +718,9 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
                                                                      const uint32_t *__restrict__ lens, uint64_t n,
                                                                      uint8_t *__restrict__ valid,
                                                                      const uint32_t *__restrict__ sidx,
-                                                                     const uint64_t *__restrict__ ooffs)
+                                                                     const uint64_t *__restrict__ ooffs, uint32_t *fault)
 {
+    using brb_line::pc_fault;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -735,7 +754,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
         Md5State st = md5_iv();
         const uint64_t nw = 16 * uint64_t(nmd);
         uint32_t cur[16], h[6] = {0, 0, 0, 0, 0, 0};
-        pair_io(
+        const bool io_ok = pair_io(
             m, nfb, nloop, src,
             [&](const uint32_t (&c)[16], uint32_t b) {
                 if (b < nfb) {
@@ -779,6 +798,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
                 for (int i = 0; i < 16; i++)
                     cur[i] = pt[i];
             });
+        if (!io_ok)
+            pc_fault(fault);
         if (live) {
             snk.flush();
             const bool tag = h[0] == 0x48534148u && (h[1] & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
@@ -828,6 +849,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
             rout[w4][j & 1][i][lane] = pt[i];
         pc_publish(m.out_cnt, j + 1);
     }
+    if (!ok)
+        pc_fault(fault);
     if (live)
         g.store(state);
 }
@@ -849,7 +872,9 @@ hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, co
     if (force >= 0)
         sector_out = force == 1;
     if (brb_opt::get(brb_opt::kRc4CryptPair) != 0 && force < 0)
-        rc4_crypt_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
+        rc4_crypt_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs,
+                                                                brb::pair_fault_word(),
+                                                                uint32_t(brb_opt::get(brb_opt::kPairStall)));
     else if (sector_out)
         rc4_crypt_kernel<true><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
     else
@@ -865,7 +890,7 @@ hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const ui
         return hipSuccess;
     if (brb_opt::get(brb_opt::kRc4Pair) != 0)
         rc4md5_frame_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n,
-                                                                   sidx);
+                                                                   sidx, brb::pair_fault_word());
     else
         rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n, sidx);
     return hipGetLastError();
@@ -878,7 +903,8 @@ hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, 
     if (n == 0)
         return hipSuccess;
     if (brb_opt::get(brb_opt::kRc4Pair) != 0)
-        rc4md5_open_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
+        rc4md5_open_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs,
+                                                                  brb::pair_fault_word());
     else
         rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
     return hipGetLastError();

@@ -25,10 +25,13 @@ enum Opt {
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
     kRc4Pair = 11,      // 1: RC4+MD5 frame / open on keystream + partner wave pairs (default); 0: one wave
     kRc4CryptPair = 12, // 1: the RC4 pass on keystream + I/O wave pairs; 0: one wave per stream does both
-    kCount = 13
+    kPairStall = 13,    // 1: inject a protocol fault into the segment-digest, MetaData and RC4-pass wave pairs
+                        // (the first workgroup's first pair never hands over its first plan / block), so the
+                        // tests see a bounded wait give up and the call report it (pair_fault.h); 0: off
+    kCount = 14
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

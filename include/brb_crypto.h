@@ -113,6 +113,13 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
 #define BRB_BATCH_PARTIAL  (-3)   /* all-devices transform batcher: some parts delivered their
                                      buffers, others could not select their device and keep their
                                      rounds pending (see Flush)                                  */
+#define BRB_BATCH_FAULT    (-4)   /* segment digests, MetaData unpack, RC4 pass, RC4+MD5 frame /
+                                     open: a wave-pair kernel's bounded wait on its partner wave
+                                     gave up (a protocol fault; never a hang).  The call's outputs,
+                                     and for RC4 the states, are wrong.  Reported by synchronous
+                                     calls only (not device-mode BRB_BATCH_ASYNC, not the
+                                     transform batcher's rounds).  Test option pair_stall injects
+                                     one.                                                        */
 
 /* flags */
 #define BRB_BATCH_HOST      0x0u   /* pointers are host memory: copied in and out by the call      */

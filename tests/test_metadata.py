@@ -254,6 +254,24 @@ def test_unpack_uniform_layouts(brb, orc, n_items, item_len, gap, seg_line):
 
 
 @pytest.mark.gpu
+def test_unpack_pair_fault_reported(brb, orc):
+    """A protocol fault in the MetaData producer / consumer pair (test option pair_stall: the first
+    pair never posts its first plan) makes the call fail with BRB_BATCH_FAULT (-4, pair_fault.h)
+    instead of returning unpack results; the next call on the same thread is clean and exact."""
+    rng = np.random.default_rng(37)
+    packs = [build([(j, i, rng.integers(0, 256, 700, dtype=np.uint8).tobytes()) for j in range(3)])
+             for i in range(300)]                         # > 46 ring words per lane: the producer blocks
+    buf, offs, lens = scatter(rng, packs)
+    with brb.TestOption("seg_line", 2), brb.TestOption("pair_stall", 1):
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.metadata_unpack_batch(buf, offs, lens)
+    with brb.TestOption("seg_line", 2):
+        got = infos_as_tuples(brb.metadata_unpack_batch(buf, offs, lens))
+    assert got == [orc.metadata_unpack(p) for p in packs]
+    assert {g[0] for g in got} == {7}
+
+
+@pytest.mark.gpu
 def test_pack_batch_round_trip(brb, orc):
     from brb_framework_amd import metadata
     rng = np.random.default_rng(5)

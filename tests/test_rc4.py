@@ -577,3 +577,25 @@ def test_frames_beyond_4gib(brb, orc, torch_dev):
         assert d[fo + 30:fo + 30 + int(lens[i])].cpu().numpy().tobytes() == payload[i], f"opened {i}"
     del words, d
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_rc4_pair_fault_reported(brb, orc, torch_dev):
+    """A protocol fault in the keystream + I/O wave pair (test option pair_stall: the first I/O wave
+    never hands a block over, so both waves' bounded waits give up) is reported as BRB_BATCH_FAULT
+    (-4, pair_fault.h) in host and device mode, never returned as a result; the next call on the
+    same thread is clean and exact."""
+    torch = torch_dev
+    n = 128
+    offs, lens, total = _layout([4096] * n)
+    data = workload.gen_records(SEED + 9, 0, 1, total)
+    states = brb.rc4_states(_keys(n, 33))
+    with brb.TestOption("rc4_pair", 1), brb.TestOption("pair_stall", 1):
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4_crypt_batch(states.copy(), data.copy(), offs, lens)
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4_crypt_batch(_to(torch, states), _to(torch, data), _to(torch, offs), _to(torch, lens))
+    st, out = states.copy(), data.copy()
+    brb.rc4_crypt_batch(st, out, offs, lens)
+    want_st, want = _oracle_crypt(orc, states, data, offs, lens)
+    assert np.array_equal(out, want) and np.array_equal(st, want_st)

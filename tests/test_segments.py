@@ -298,3 +298,30 @@ def test_segments_beyond_4gib(brb, torch_dev, seg_line):
         assert got[i].tobytes() == hashlib.md5(msg).digest(), i
     del words, d
     t.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_segments_pair_fault_reported(brb, torch_dev, device):
+    """A protocol fault in the producer / consumer pair (test option pair_stall: the first pair never
+    posts its first plan, so the consumer's and then the producer's bounded waits give up) makes the
+    call fail with BRB_BATCH_FAULT (-4, pair_fault.h) instead of returning digests; the next call on
+    the same thread is clean and equals hashlib."""
+    t = torch_dev
+    n = 256
+    pool = workload.gen_records(0x5EED00FB, 0, 1, 1 << 20)
+    rng = np.random.default_rng(47)
+    first = (np.arange(n + 1, dtype=np.uint64) * 2).astype(np.uint64)
+    lens = rng.integers(600, 1200, 2 * n).astype(np.uint32)      # > 46 ring words per lane: the producer blocks
+    offs = rng.integers(0, (1 << 20) - 1200, 2 * n).astype(np.uint64)
+    args = (pool, offs, lens, first)
+    if device:
+        args = tuple(t.from_numpy(np.ascontiguousarray(a)).cuda() for a in args)
+    with brb.TestOption("seg_line", 2), brb.TestOption("pair_stall", 1):
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.md5_batch_segments(*args)
+    with brb.TestOption("seg_line", 2):
+        got = brb.md5_batch_segments(*args)
+    got = got.cpu().numpy() if device else got
+    for i in range(n):
+        msg = b"".join(pool[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes() for k in (2 * i, 2 * i + 1))
+        assert got[i].tobytes() == hashlib.md5(msg).digest(), i
