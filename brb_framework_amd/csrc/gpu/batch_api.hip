@@ -103,7 +103,7 @@ namespace brb_api {
 // (an event thread that ends returns its HBM) or by BRB_CryptoGPU_ThreadCleanup().
 struct Workspaces {
     std::vector<std::pair<void *, size_t>> by_dev;   // (ptr, capacity) per device ordinal
-    std::vector<uint32_t *> fault_by_dev;             // pair_fault.h: the thread's fault word per device
+    uint32_t *fault_word = nullptr;                   // pair_fault.h: the thread's fault word
     void release()
     {
         for (size_t d = 0; d < by_dev.size(); d++)
@@ -112,38 +112,33 @@ struct Workspaces {
                 (void)hipFree(by_dev[d].first);
                 by_dev[d] = {nullptr, 0};
             }
-        for (uint32_t *&w : fault_by_dev)
-            if (w) {
-                (void)hipHostFree(w);
-                w = nullptr;
-            }
+        if (fault_word) {
+            (void)hipHostFree(fault_word);
+            fault_word = nullptr;
+        }
     }
     ~Workspaces() { release(); }
 };
 thread_local Workspaces t_ws;
 thread_local uint32_t *t_fault_armed = nullptr;       // the word the pair kernels' launchers pass
 
-// The calling thread's fault word on the current device: page-locked, device-mapped, coherent host
-// memory (the kernel's store is visible once the stream has drained).  nullptr if it cannot be had.
+// The calling thread's fault word: page-locked, device-mapped, coherent host memory, portable to
+// every device (one word serves the thread whatever device it calls on; the kernel's store is visible
+// once the stream has drained).  Allocated on the thread's first armed call; nullptr if it cannot be
+// had.  The word is 0 between calls (check() clears it), so arming a call is one thread-local store
+// and nothing runs between the caller and the launch (the bench's events see no host work).
 uint32_t *fault_word()
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    if (t_ws.fault_by_dev.size() <= size_t(dev))
-        t_ws.fault_by_dev.resize(dev + 1, nullptr);
-    uint32_t *&w = t_ws.fault_by_dev[dev];
-    if (!w) {
+    if (!t_ws.fault_word) {
         void *p = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }
-        w = static_cast<uint32_t *>(p);
+        t_ws.fault_word = static_cast<uint32_t *>(p);
+        *t_ws.fault_word = 0;
     }
-    return w;
+    return t_ws.fault_word;
 }
 
 // Arms the thread's fault word for one synchronous call (pair_fault.h); check() after the stream
@@ -155,17 +150,17 @@ struct PairFault {
         if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC))
             return;
         w = fault_word();
-        if (w) {
-            __atomic_store_n(w, 0u, __ATOMIC_RELAXED);
-            t_fault_armed = w;
-        }
+        t_fault_armed = w;
     }
     ~PairFault() { t_fault_armed = nullptr; }
     PairFault(const PairFault &) = delete;
     PairFault &operator=(const PairFault &) = delete;
     int check(int rc) const
     {
-        if (rc != BRB_BATCH_OK || !w || __atomic_load_n(w, __ATOMIC_ACQUIRE) == 0)
+        if (!w || __atomic_load_n(w, __ATOMIC_ACQUIRE) == 0)
+            return rc;
+        __atomic_store_n(w, 0u, __ATOMIC_RELAXED);      // clean for the thread's next call
+        if (rc != BRB_BATCH_OK)
             return rc;
         set_err("wave-pair protocol fault: a kernel's bounded wait on its partner wave gave up; the "
                 "outputs (and RC4 states) of this call are wrong");

@@ -354,12 +354,14 @@ __global__ __launch_bounds__(64 * W) void md5_seg_line_kernel(const uint8_t *__r
 // group's plan (K lines, or 0: the per-lane path, run by the producer alone) and its end (the carried
 // bytes and the length in `fin`); the consumer acknowledges the plan and, after the digest, the end
 // (its cpos back to 0).  A producer starts a group only once every earlier event is acknowledged.
-template <int NP>
+// STALL: test option pair_stall (pair_fault.h), a separate instantiation so the product kernel
+// carries no test code.
+template <int NP, bool STALL>
 __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ soff,
                                                              const uint32_t *__restrict__ slen,
                                                              const uint64_t *__restrict__ first, uint64_t n_rec,
-                                                             uint8_t *__restrict__ out, uint32_t *fault, uint32_t stall)
+                                                             uint8_t *__restrict__ out, uint32_t *fault)
 {
     using namespace brb_line;
     constexpr uint32_t RW = 64;                         // funnel ring words per lane (16 KiB per pair)
@@ -371,10 +373,13 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     __shared__ uint32_t wpx[NP][64], cpx[NP][64];       // the mailboxes: words written, words compressed
     __shared__ uint32_t fin[NP][3][64];                 // carried bytes | count << 24, length lo / hi
     __shared__ uint32_t ev[NP][4];                      // producer events, consumer events, plan, heartbeat
+    __shared__ uint32_t *fault_at;                      // pair_sync.h pc_fault_from
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pr = wv % NP;
     const bool producer = wv < NP;
+    if (threadIdx.x == 0)
+        fault_at = fault;
     if (threadIdx.x < NP * 4)
         (&ev[0][0])[threadIdx.x] = 0;
     if (threadIdx.x < NP * 64) {
@@ -394,7 +399,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
 #endif
         for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
             if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3])) {
-                pc_fault(fault);
+                pc_fault_from(&fault_at);
                 return;
             }
             pseen++;
@@ -406,12 +411,12 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             f.init(&fring[pr][0][lane]);
 #ifdef BRB_LINE_STAMPS
             if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3], &c_wait)) {
-                pc_fault(fault);
+                pc_fault_from(&fault_at);
                 return;
             }
 #else
             if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3])) {
-                pc_fault(fault);
+                pc_fault_from(&fault_at);
                 return;
             }
 #endif
@@ -450,10 +455,8 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
     const uint64_t p_t0 = __builtin_amdgcn_s_memtime();
 #endif
     for (uint64_t g = uint64_t(blockIdx.x) * NP + pr; g < n_groups; g += gstride) {
-        if (!pc_wait_ge(&ev[pr][1], cexp)) {           // every earlier event acknowledged
-            pc_fault(fault);
-            return;
-        }
+        if (!pc_wait_ge(&ev[pr][1], cexp))             // every earlier event acknowledged (a fault: the
+            return;                                     // consumer, waiting on this wave, reports it)
         const uint64_t rec = g * 64 + lane;
         const bool valid = rec < n_rec;
         const uint64_t k0 = valid ? first[rec] : 0, k1 = valid ? first[rec + 1] : 0;
@@ -476,7 +479,7 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
         const uint32_t K = sg.K;
         wpx[pr][lane] = 0;                              // the consumer reads it only after the plan
         ev[pr][2] = K;                                  // the plan (K >= 1)
-        if (stall && blockIdx.x == 0 && pr == 0 && pev == 0)
+        if (STALL && blockIdx.x == 0 && pr == 0 && pev == 0)
             ++pev;                                      // test option pair_stall: the plan is never posted
         else
             pc_publish(&ev[pr][0], ++pev);
@@ -536,10 +539,8 @@ __global__ __launch_bounds__(128 * NP) void md5_seg_pc_kernel(const uint8_t *__r
             sa = sb;
         }
         brb_dma::wait_vmcnt<0>();                       // the stray stage past K, before the slots are reused
-        if (!ok) {
-            pc_fault(fault);
-            return;
-        }
+        if (!ok)
+            return;                                     // reported by the consumer (it stops getting words)
         fin[pr][0][lane] = uint32_t(f.acc) | (f.nacc << 24);
         fin[pr][1][lane] = uint32_t(f.total);
         fin[pr][2][lane] = uint32_t(f.total >> 32);
@@ -571,8 +572,10 @@ hipError_t launch_md5_segments(const uint8_t *data, const uint64_t *soff, const 
         constexpr int NP = 4;                          // 4 pairs, 159 KiB of LDS: one workgroup per CU
         const uint64_t wgs = (groups + NP - 1) / NP;
         const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-        md5_seg_pc_kernel<NP><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out, brb::pair_fault_word(),
-                                                        uint32_t(brb_opt::get(brb_opt::kPairStall)));
+        if (brb_opt::get(brb_opt::kPairStall) != 0)
+            md5_seg_pc_kernel<NP, true><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out, brb::pair_fault_word());
+        else
+            md5_seg_pc_kernel<NP, false><<<grid, 128 * NP, 0, s>>>(data, soff, slen, first, n_rec, out, brb::pair_fault_word());
         return hipGetLastError();
     }
     constexpr int W = 4;                               // 4 x (8 NS + 14) KiB of LDS: one workgroup per CU

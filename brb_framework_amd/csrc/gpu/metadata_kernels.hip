@@ -190,12 +190,13 @@ __global__ __launch_bounds__(kBlock) void metadata_unpack_kernel(const uint8_t *
 // wave (the producer) emits the words into the pair's 64-word ring; its partner on the same SIMD
 // (wave W + p) compresses them, pads, checks the digest and writes the info (two ring slots, so that
 // four pairs fit a CU's LDS).
-template <int W, int NS, bool PC>
+// STALL: test option pair_stall (pair_fault.h), PC only.
+template <int W, int NS, bool PC, bool STALL = false>
 __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(const uint8_t *__restrict__ data,
                                                                                const uint64_t *__restrict__ offs,
                                                                                const uint32_t *__restrict__ lens, uint64_t n,
                                                                                BRB_MetaDataUnpackInfo *__restrict__ info,
-                                                                               uint32_t *fault, uint32_t stall)
+                                                                               uint32_t *fault)
 {
     using namespace brb_line;
     constexpr uint32_t RW = PC ? 64 : brb_line::kRingWords;
@@ -208,12 +209,15 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
     __shared__ uint32_t wpx[WP][64], cpx[WP][64];       // pairs: words written, words compressed
     __shared__ uint32_t fin[WP][15][64];                // pairs: the walk's results for the consumer
     __shared__ uint32_t ev[WP][4];                      // pairs: producer events, consumer events, plan, heartbeat
+    __shared__ uint32_t *fault_at;                      // pairs: pair_sync.h pc_fault_from
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pr = PC ? wv % W : wv;
     const uint64_t n_groups = (n + 63) / 64;
     const uint64_t gstride = uint64_t(gridDim.x) * W;
     if (PC) {
+        if (threadIdx.x == 0)
+            fault_at = fault;
         if (threadIdx.x < WP * 4)
             (&ev[0][0])[threadIdx.x] = 0;
         if (threadIdx.x < WP * 64) {
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
         uint32_t pseen = 0, cev = 0;
         for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
             if (!pc_wait_ge(&ev[pr][0], pseen + 1, &ev[pr][3])) {
-                pc_fault(fault);
+                pc_fault_from(&fault_at);
                 return;
             }
             pseen++;
@@ -238,7 +242,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
             brb_md5::FunnelT<RW> f;
             f.init(&fring[pr][0][lane]);
             if (!pc_consume(f, &ev[pr][0], pseen + 1, &wpx[pr][lane], &cpx[pr][lane], &ev[pr][3])) {
-                pc_fault(fault);
+                pc_fault_from(&fault_at);
                 return;
             }
             pseen++;
@@ -281,10 +285,8 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
     uint32_t beats = 0;                                 // pairs: heartbeat, one per line
 
     for (uint64_t g = uint64_t(blockIdx.x) * W + pr; g < n_groups; g += gstride) {
-        if (PC && !pc_wait_ge(&ev[pr][1], cexp)) {      // every earlier event acknowledged
-            pc_fault(fault);
-            return;
-        }
+        if (PC && !pc_wait_ge(&ev[pr][1], cexp))        // every earlier event acknowledged (a fault: the
+            return;                                       // consumer, waiting on this wave, reports it)
         const uint64_t r = g * 64 + lane;
         const bool valid = r < n;
         const uint64_t base = valid ? dbase + offs[r] : dbase;
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
         if (PC) {
             *my_wpx = 0;                                  // the consumer reads it only after the plan
             ev[pr][2] = K;
-            if (stall && blockIdx.x == 0 && pr == 0 && pev == 0)
+            if (STALL && blockIdx.x == 0 && pr == 0 && pev == 0)
                 ++pev;                                    // test option pair_stall: the plan is never posted
             else
                 pc_publish(&ev[pr][0], ++pev);
@@ -464,10 +466,8 @@ __global__ __launch_bounds__(64 * W * (PC ? 2 : 1)) void metadata_line_kernel(co
             }
         }
         brb_dma::wait_vmcnt<0>();                                // the stray stages, before the slots are reused
-        if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0) {
-            pc_fault(fault);                                     // a protocol fault: reported, no hang
-            return;
-        }
+        if (PC && __builtin_amdgcn_ballot_w64(!ok) != 0)
+            return;                                              // a protocol fault: the consumer reports it
         if (phase != kDone) {                                    // a pack shorter than its header
             uint32_t dw[36] = {};
             events(int64_t(1) << 62, int64_t(1) << 62, 0, 0, dw, true);
@@ -517,15 +517,18 @@ hipError_t launch_metadata_unpack(const uint8_t *data, const uint64_t *offs, con
     const uint64_t groups = (n + 63) / 64;
     const uint64_t wgs = (groups + W - 1) / W;
     const unsigned grid = unsigned(wgs < brb_digest::device_cu_count() ? wgs : brb_digest::device_cu_count());
-    if (brb_opt::get(brb_opt::kSegLine) == 2)          // wave pairs
-        metadata_line_kernel<W, 2, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info, brb::pair_fault_word(),
-                                                                  uint32_t(brb_opt::get(brb_opt::kPairStall)));
-    // three slots by default: 43.6 vs 49.3 us with two (bench --op metadata, interleaved A/B,
-    // gpurun_out/r04s_md); test option line_slots 2 for the other
-    else if (brb_opt::get(brb_opt::kLineSlots) == 2)
-        metadata_line_kernel<W, 2, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr, 0u);
-    else
-        metadata_line_kernel<W, 3, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr, 0u);
+    if (brb_opt::get(brb_opt::kSegLine) == 2) {        // wave pairs
+        if (brb_opt::get(brb_opt::kPairStall) != 0)
+            metadata_line_kernel<W, 2, true, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info, brb::pair_fault_word());
+        else
+            metadata_line_kernel<W, 2, true><<<grid, 128 * W, 0, s>>>(data, offs, lens, n, info, brb::pair_fault_word());
+    } else if (brb_opt::get(brb_opt::kLineSlots) == 2) {
+        // three slots by default: 43.6 vs 49.3 us with two (bench --op metadata, interleaved A/B,
+        // profiles/r04/ab/r04s_md); test option line_slots 2 for the other
+        metadata_line_kernel<W, 2, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr);
+    } else {
+        metadata_line_kernel<W, 3, false><<<grid, 64 * W, 0, s>>>(data, offs, lens, n, info, nullptr);
+    }
     return hipGetLastError();
 }
 

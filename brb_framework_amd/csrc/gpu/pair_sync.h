@@ -68,8 +68,20 @@ BRB_DEV void pc_publish(uint32_t *ctr, uint32_t v)
 // has completed.
 BRB_DEV void pc_fault(uint32_t *fault)
 {
-    if (fault)
-        __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (fault)   // a global (not flat) store: no flat access anywhere in the pair kernels
+        __hip_atomic_store((__attribute__((address_space(1))) uint32_t *)fault, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The pair kernels keep the fault word's address in LDS (`fault_at`, written by thread 0 before the
+// kernel's first barrier) and read it back only when a wait gives up: a kernel argument live for the
+// whole kernel holds an SGPR pair (md5_seg_pc_kernel: SGPR spills 39 -> 47).  Both accesses are
+// typed (ds_read, global_store): a generic pointer made them flat_load / flat_store, and one flat
+// access in these LDS-heavy kernels made hipcc's wait-count insertion conservative everywhere --
+// md5seg 34.3 -> 35.1 us, MetaData 38.5 -> 38.9 us, with the flat ops on cold paths only.
+BRB_DEV void pc_fault_from(uint32_t **fault_at)
+{
+    pc_fault(__hip_atomic_load(fault_at, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 
 }  // namespace brb_line

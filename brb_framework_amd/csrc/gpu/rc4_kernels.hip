@@ -342,14 +342,16 @@ BRB_DEV bool rc4_wait(F blocked)
     return false;
 }
 
+// STALL: test option pair_stall (pair_fault.h), a separate instantiation so the product kernel
+// carries no test code.
+template <bool STALL>
 __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__restrict__ states, const uint8_t *in,
                                                                    uint8_t *out, const uint64_t *__restrict__ offs,
                                                                    const uint32_t *__restrict__ lens, uint64_t n,
                                                                    const uint32_t *__restrict__ sidx,
-                                                                   const uint64_t *__restrict__ ooffs, uint32_t *fault,
-                                                                   uint32_t stall)
+                                                                   const uint64_t *__restrict__ ooffs, uint32_t *fault)
 {
-    using brb_line::pc_fault;
+    using brb_line::pc_fault_from;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -357,11 +359,14 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
     __shared__ uint32_t rout[kWaves][2][16][64];        // produced output blocks
     __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
     __shared__ uint32_t mb[kWaves][4][64];              // staged, taken, produced, stored (blocks)
+    __shared__ uint32_t *fault_at;                      // pair_sync.h pc_fault_from
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t w4 = wv % kWaves;
     for (uint32_t i = threadIdx.x; i < kWaves * 4 * 64; i += 2 * kWave)
         (&mb[0][0][0])[i] = 0;
+    if (threadIdx.x == 0)
+        fault_at = fault;
     __syncthreads();
     const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
     const bool live = s < n;                           // lanes past n only help with the block loads
@@ -377,7 +382,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
         Snk snk;
         snk.init(out + (live && ooffs ? ooffs[s] : off), len);
         // test option pair_stall: the first workgroup's first I/O wave never hands a block over
-        const bool stalled = stall && blockIdx.x == 0 && w4 == 0;
+        const bool stalled = STALL && blockIdx.x == 0 && w4 == 0;
         uint32_t bi = 0, bo = 0;
         for (uint32_t idle = 0; bo < nloop && idle < (1u << 22);) {
             // stage block bi once the keystream wave has taken block bi - 2 (its slot is free)
@@ -419,7 +424,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
             idle++;
         }
         if (bo < nloop)
-            pc_fault(fault);                           // a protocol fault: reported, never a hang
+            pc_fault_from(&fault_at);                 // a protocol fault: reported, never a hang
         if (live)
             snk.flush();
         return;
@@ -433,10 +438,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
     if (live)
         g.load(state);
     for (uint32_t b = 0; b < nloop; b++) {
-        if (!rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; })) {
-            pc_fault(fault);                           // a protocol fault: reported, never a hang
-            break;
-        }
+        if (!rc4_wait([&] { return b < nblk && pc_load(m.in_cnt) < b + 1; }))
+            break;                                     // a protocol fault: the I/O wave reports it
         if (b >= nblk)
             continue;
         uint32_t c[16];
@@ -459,10 +462,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4_crypt_pair_kernel(uint8_t *__re
                 o[i] = q < len ? c[i] ^ g.next_n(clamp4(len - q)) : 0u;
             }
         }
-        if (!rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; })) {
-            pc_fault(fault);
+        if (!rc4_wait([&] { return pc_load(m.out_used) + 2 <= b; }))
             break;
-        }
 #pragma unroll
         for (int i = 0; i < 16; i++)
             rout[w4][b & 1][i][lane] = o[i];
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
                                                                       const uint64_t *__restrict__ foffs, uint64_t n,
                                                                       const uint32_t *__restrict__ sidx, uint32_t *fault)
 {
-    using brb_line::pc_fault;
+    using brb_line::pc_fault_from;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -536,6 +537,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
     __shared__ uint32_t rout[kWaves][2][16][64];
     __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
     __shared__ uint32_t mb[kWaves][4][64];
+    __shared__ uint32_t *fault_at;                      // pair_sync.h pc_fault_from
     __shared__ uint32_t dg[kWaves][4][64];        // the digests
     __shared__ uint32_t posted[kWaves];
     const uint32_t lane = threadIdx.x & 63;
@@ -545,6 +547,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
         (&mb[0][0][0])[i] = 0;
     if (threadIdx.x < kWaves)
         posted[threadIdx.x] = 0;
+    if (threadIdx.x == 0)
+        fault_at = fault;
     __syncthreads();
     const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
     const bool live = s < n;
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
                 }
             });
         if (!io_ok)
-            pc_fault(fault);
+            pc_fault_from(&fault_at);
         if (nloop == 0)
             pc_publish(&posted[w4], 1u);
         if (live)
@@ -680,8 +684,6 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
             rout[w4][b & 1][i][lane] = ct[i];
         pc_publish(m.out_cnt, b + 1);
     }
-    if (!ok)
-        pc_fault(fault);
     if (!live)
         return;
     const bool got = brb_line::pc_wait_ge(&posted[w4], 1u) && ok;
@@ -690,10 +692,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
     st.b = dg[w4][1][lane];
     st.c = dg[w4][2][lane];
     st.d = dg[w4][3][lane];
-    if (!got) {
-        st.a = ~st.a;                             // a protocol fault: a wrong header, reported, never a hang
-        pc_fault(fault);
-    }
+    if (!got)
+        st.a = ~st.a;                             // a protocol fault (a wrong header; the partner reports it)
     const uint64_t salt = salts[s];
     uint32_t h[8];
     h[0] = uint32_t(salt);
@@ -720,7 +720,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
                                                                      const uint32_t *__restrict__ sidx,
                                                                      const uint64_t *__restrict__ ooffs, uint32_t *fault)
 {
-    using brb_line::pc_fault;
+    using brb_line::pc_fault_from;
     using brb_line::pc_load;
     using brb_line::pc_publish;
     __shared__ __attribute__((aligned(16))) uint8_t slot[kSlotLds];
@@ -728,11 +728,14 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
     __shared__ uint32_t rout[kWaves][2][16][64];
     __shared__ __attribute__((aligned(16))) uint8_t xch[kWaves * kXchBytes];
     __shared__ uint32_t mb[kWaves][4][64];
+    __shared__ uint32_t *fault_at;                      // pair_sync.h pc_fault_from
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t w4 = wv % kWaves;
     for (uint32_t i = threadIdx.x; i < kWaves * 4 * 64; i += 2 * kWave)
         (&mb[0][0][0])[i] = 0;
+    if (threadIdx.x == 0)
+        fault_at = fault;
     __syncthreads();
     const uint64_t s = uint64_t(blockIdx.x) * kWave + w4 * 64 + lane;
     const bool live = s < n;
@@ -799,7 +802,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
                     cur[i] = pt[i];
             });
         if (!io_ok)
-            pc_fault(fault);
+            pc_fault_from(&fault_at);
         if (live) {
             snk.flush();
             const bool tag = h[0] == 0x48534148u && (h[1] & 0xFFu) == 0x3Au;   // "HASH:" at 8..12
@@ -849,8 +852,6 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
             rout[w4][j & 1][i][lane] = pt[i];
         pc_publish(m.out_cnt, j + 1);
     }
-    if (!ok)
-        pc_fault(fault);
     if (live)
         g.store(state);
 }
@@ -871,11 +872,14 @@ hipError_t launch_rc4_crypt(uint8_t *states, const uint8_t *in, uint8_t *out, co
     const int force = brb_opt::get(brb_opt::kRc4Sector);
     if (force >= 0)
         sector_out = force == 1;
-    if (brb_opt::get(brb_opt::kRc4CryptPair) != 0 && force < 0)
-        rc4_crypt_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs,
-                                                                brb::pair_fault_word(),
-                                                                uint32_t(brb_opt::get(brb_opt::kPairStall)));
-    else if (sector_out)
+    if (brb_opt::get(brb_opt::kRc4CryptPair) != 0 && force < 0) {
+        if (brb_opt::get(brb_opt::kPairStall) != 0)
+            rc4_crypt_pair_kernel<true><<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs,
+                                                                          brb::pair_fault_word());
+        else
+            rc4_crypt_pair_kernel<false><<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs,
+                                                                           brb::pair_fault_word());
+    } else if (sector_out)
         rc4_crypt_kernel<true><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
     else
         rc4_crypt_kernel<false><<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, sidx, ooffs);
