@@ -401,7 +401,8 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * "line_slots" 0/2/3 (LDS-DMA ring slots of the line-staged segment and MetaData kernels: each
  * kernel's default, or forced), "rc4md5_pair" 1/0 (BRB_RC4MD5_FrameBatch / OpenBatch on keystream +
  * partner wave pairs / one wave per connection), "rc4_pair" 1/0 (BRB_RC4_CryptBatch likewise; a forced
- * "rc4_sector" value selects the one-wave kernel).  Returns 1 and the previous
+ * "rc4_sector" value selects the one-wave kernel), "pair_stall" 0/1 (1: the segment, MetaData and RC4
+ * pass wave pairs get a protocol fault injected, so the call returns BRB_BATCH_FAULT).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */
