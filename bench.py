@@ -26,6 +26,7 @@ import hashlib
 import json
 import math
 import os
+import re
 import subprocess
 import sys
 import time
@@ -121,22 +122,99 @@ def core_counts(threads: int, single_core_rate: float) -> dict:
                           "all_affinity_cpus_extrapolated = single-core rate x affinity CPUs, not measured"}
 
 
-def load_pmc(path, key):
-    """(traffic bytes, detail dict) measured by rocprofv3 --pmc for `key`, or (None, None)."""
+def kernel_id(name: str) -> str:
+    """A rocprofv3 kernel name without `void`, namespaces and the argument list: the kernel and its
+    template arguments, e.g. "rc4_crypt_pair_kernel<false>", "digest_line_kernel<Md5Alg, 8, true,
+    true, true>".  tools/collect_profiles.py records these in pmc_traffic.json."""
+    n = name.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    n = n.replace("(anonymous namespace)::", "")
+    depth = 0
+    for i, ch in enumerate(n):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            n = n[:i]
+            break
+    return re.sub(r"\b[A-Za-z_]\w*::", "", n).strip()
+
+
+def timed_kernel_patterns(key, opt):
+    """Regexes (on kernel_id) of the kernels one step of bench line `key` launches, as the launchers
+    in csrc/gpu/*.hip select them under the current test options (`opt(name)` reads one), one regex
+    per kernel of the step.  None for a key without PMC evidence."""
+    seg = opt("seg_line")
+    rc4_pair = opt("rc4_pair") != 0 and opt("rc4_sector") < 0
+    table = {
+        "cfg2_md5": [r"digest_line_kernel<Md5Alg, .*>"],
+        "cfg2_sha1": [r"digest_line_kernel<Sha1Alg, .*>"],
+        "cfg3_md5": [r"digest_b64r_kernel<Md5Alg, .*>"],
+        "cfg4_blowfish": [r"bf_rep_kernel<\d+, false>", r"bf_rep_kernel<\d+, true>"],
+        "f1_rc4": [r"rc4_crypt_pair_kernel<false>"] if rc4_pair else [r"rc4_crypt_kernel<(true|false)>"],
+        "f1_rc4md5": ([r"rc4md5_frame_pair_kernel<false>", r"rc4md5_open_pair_kernel<false>"] if opt("rc4md5_pair")
+                      else [r"rc4md5_frame_kernel(<.*>)?", r"rc4md5_open_kernel(<.*>)?"]),
+        "f4_metadata": {2: [r"metadata_line_kernel<\d+, \d+, true, false>"],
+                        1: [r"metadata_line_kernel<\d+, \d+, false, false>"],
+                        0: [r"metadata_unpack_kernel"]}[seg],
+        "f4_md5seg": {2: [r"md5_seg_pc_kernel<\d+, false>"], 1: [r"md5_seg_line_kernel<\d+, \d+>"],
+                      0: [r"md5_seg_kernel"]}[seg],
+        "f4_base64": [r"b64_encode_group_kernel", r"b64_decode_group_kernel"],
+        "var_md5var": [r"digest_var_line_kernel<Md5Alg, .*>"] if opt("var_line") else [r"md5_any_kernel<.*>"],
+        "var_sha1var": [r"digest_var_line_kernel<Sha1Alg, .*>"] if opt("var_line") else [r"sha1_any_kernel<.*>"],
+    }
+    return table.get(key)
+
+
+def kernels_match(pmc_kernels, patterns) -> bool:
+    """Every kernel of the PMC pass is one the timed region launches, and every kernel the timed
+    region launches was profiled (one to one)."""
+    if not pmc_kernels or not patterns or len(pmc_kernels) != len(patterns):
+        return False
+    left = list(pmc_kernels)
+    for p in patterns:
+        hit = next((k for k in left if re.fullmatch(p, k)), None)
+        if hit is None:
+            return False
+        left.remove(hit)
+    return not left
+
+
+OPT = None   # set by main(): reads a BRB_CryptoGPU_TestOption value
+
+
+def load_pmc(path, key, opt=None):
+    """(traffic bytes, detail dict, refusal) measured by rocprofv3 --pmc for `key`.  The entry is
+    used only if the kernels it profiled ("kernels", kernel_id form) are the ones this line's timed
+    region launches (timed_kernel_patterns under the current test options): otherwise (None, None,
+    reason) -- a line never carries another kernel's traffic or bound."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(key), d.get(key + "_detail")
     except (OSError, ValueError):
-        return None, None
+        return None, None, "no PMC summary"
+    det = d.get(key + "_detail")
+    if det is None:
+        return None, None, f"no PMC entry {key}"
+    opt = opt or OPT
+    pats = timed_kernel_patterns(key, opt) if opt else None
+    got = det.get("kernels")
+    if pats is None or not kernels_match(got, pats):
+        return None, None, (f"PMC entry {key} ({det.get('source')}) profiled {got}, the timed region launches "
+                            f"{pats}: not used")
+    return d.get(key), det, None
 
 
 def traffic_fields(path, key, per_step=1):
-    t, det = load_pmc(path, key)
-    src = (det or {}).get("source")
+    t, det, why = load_pmc(path, key)
+    if why:
+        return {"traffic": None, "traffic_source": why}
+    src = det.get("source")
     return {"traffic": t * per_step if t else None,
-            "traffic_source": (f"{src}: rocprofv3 --pmc passes of an earlier run (tools/gpu_pmc.sh), not this run"
-                               if src else None)}
+            "traffic_source": (f"{src}: rocprofv3 --pmc passes of an earlier run (tools/gpu_pmc.sh), not this run; "
+                               f"kernels {det.get('kernels')}")}
 
 
 def compute_fraction(path, key, launch_s, cyc_lone):
@@ -147,15 +225,17 @@ def compute_fraction(path, key, launch_s, cyc_lone):
     compression at one wave per SIMD (tools/mb/md5_occ.hip).  That cost is close to the SIMD's
     rate for the mix at any wave count (4.30 / 4.11 / 4.03 cycles at 1 / 2 / 4 waves per SIMD),
     so it is the compute ceiling of cfg3/cfg5 too."""
-    _, det = load_pmc(path, key)
-    if not det or "sq_insts_valu" not in det:
+    _, det, why = load_pmc(path, key)
+    if why:
+        return {"refused": why}
+    if "sq_insts_valu" not in det:
         return None
     per_simd = det["sq_insts_valu"] / SIMDS
     cyc = launch_s * CLOCK_GHZ * 1e9
     out = {"bound": "valu-issue", "sq_insts_valu_per_launch": det["sq_insts_valu"],
            "valu_per_simd": round(per_simd, 1), "clock_ghz": CLOCK_GHZ,
            "peak_cycles_per_inst": VALU_PEAK_CYC, "frac_peak": round(per_simd * VALU_PEAK_CYC / cyc, 4),
-           "source": det.get("source")}
+           "source": det.get("source"), "kernels": det.get("kernels")}
     if cyc_lone:
         out["lone_wave_cycles_per_inst"] = cyc_lone
         out["frac_lone_wave"] = round(per_simd * cyc_lone / cyc, 4)
@@ -182,8 +262,10 @@ def issue_compute(path, key, launch_s, dispatches=1):
                        cycles each SIMD had a wave issuing (clock-free);
       wait_frac / wait_inst_frac  SQ_WAIT_ANY / SQ_WAVE_CYCLES (waiting on memory or LDS data) and
                        SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waiting for an issue slot)."""
-    _, det = load_pmc(path, key)
-    if not det or "sq_insts_valu" not in det:
+    _, det, why = load_pmc(path, key)
+    if why:
+        return {"refused": why}
+    if "sq_insts_valu" not in det:
         return None
     per_launch = launch_s / dispatches
     insts = det["sq_insts_valu"] + det.get("sq_insts_lds", 0) + det.get("sq_insts_salu", 0)
@@ -194,7 +276,7 @@ def issue_compute(path, key, launch_s, dispatches=1):
            "valu_per_simd": round(det["sq_insts_valu"] / SIMDS, 1), "waves_per_simd": round(wps, 2),
            "cycles_per_inst": cyc, "clock_ghz": CLOCK_GHZ,
            "frac_issue_ceiling": round(per_simd * cyc / (per_launch * CLOCK_GHZ * 1e9), 4),
-           "source": det.get("source")}
+           "source": det.get("source"), "kernels": det.get("kernels")}
     if "sq_active_inst_any" in det and det.get("grbm_gui_active"):
         out["issue_busy_frac"] = round(det["sq_active_inst_any"] * 4 / SIMDS / (det["grbm_gui_active"] / 8), 4)
     if det.get("sq_wave_cycles"):
@@ -239,7 +321,13 @@ def main():
     for opt in args.test_option:
         name, value = opt.split("=")
         brb.test_option(name, int(value))
-    global MARK
+
+    def opt_value(name):
+        old = brb.test_option(name, 0)     # every option's range holds 0
+        brb.test_option(name, old)
+        return old
+    global MARK, OPT
+    OPT = opt_value
     MARK = args.mark_timed_region
 
     def barrier():
@@ -741,15 +829,17 @@ def blowfish_compute(path):
     MI355X_MICROARCH.md "DVFS give-back"), so lds_busy_frac = (IDX_ACTIVE / 256) / (GUI_ACTIVE / 8)
     with no clock assumption; valu_frac_peak = SQ_INSTS_VALU / 1024 SIMDs x 2 cycles over the same
     cycles."""
-    _, det = load_pmc(path, "cfg4_blowfish")
-    if not det or "sq_lds_idx_active" not in det or "grbm_gui_active" not in det:
+    _, det, why = load_pmc(path, "cfg4_blowfish")
+    if why:
+        return {"refused": why}
+    if "sq_lds_idx_active" not in det or "grbm_gui_active" not in det:
         return None
     cyc = det["grbm_gui_active"] / 8
     out = {"bound": "simd-issue, then lds-gather", "dispatch_cycles": round(cyc),
            "lds_busy_frac": round(det["sq_lds_idx_active"] / 256 / cyc, 4),
            "lds_bank_conflict_frac": round(det.get("sq_lds_bank_conflict", 0) / 256 / cyc, 4),
            "valu_frac_peak": round(det["sq_insts_valu"] / SIMDS * VALU_PEAK_CYC / cyc, 4),
-           "source": det.get("source")}
+           "source": det.get("source"), "kernels": det.get("kernels")}
     if "sq_active_inst_any" in det:
         # SQ_ACTIVE_INST_ANY: quad-cycles in which a wave issued, summed over waves; x 4 / 1024 SIMDs
         # = the cycles each SIMD spent issuing (4 waves per SIMD here, at most one issuing at a time)

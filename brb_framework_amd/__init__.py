@@ -17,6 +17,7 @@ from .crypto import (  # noqa: F401
     TRANSFORM_DROPPED,
     TestOption,
     test_option,
+    async_fault_check,
     BATCH_ASYNC,
     BATCH_DEVICE,
     BATCH_HOST,
@@ -74,5 +75,5 @@ __all__ = [
     "membuf_encrypt", "membuf_key", "membuf_span", "md5_batch_segments", "metadata_unpack_batch", "METADATA_INFO_DTYPE", "base64_decode_batch",
     "base64_encode_batch", "CRYPTO_FUNC_RC4", "CRYPTO_FUNC_RC4_MD5", "OP_READ", "OP_WRITE", "TransformBatcher",
     "HostRegion", "BATCHER_ZERO_COPY", "BATCHER_PIPELINED", "BATCH_ALL_DEVICES", "device_count",
-    "BATCH_DROPPED", "TRANSFORM_DROPPED", "BATCHER_ALL_DEVICES", "TestOption", "test_option",
+    "BATCH_DROPPED", "TRANSFORM_DROPPED", "BATCHER_ALL_DEVICES", "TestOption", "test_option", "async_fault_check",
 ]

@@ -141,6 +141,7 @@ _SIGNATURES = [
     ("BRB_CryptoGPU_GetDevice", ctypes.c_int, []),
     ("BRB_CryptoGPU_ThreadCleanup", None, []),
     ("BRB_CryptoGPU_LastError", ctypes.c_char_p, []),
+    ("BRB_CryptoGPU_AsyncFaultCheck", ctypes.c_int, []),
     ("BRB_CryptoGPU_Version", ctypes.c_char_p, []),
 ]
 
@@ -188,6 +189,12 @@ def exported_symbols() -> set:
 
 def gpu_available() -> bool:
     return bool(lib().BRB_CryptoGPU_Available())
+
+
+def async_fault_check() -> None:
+    """BRB_CryptoGPU_AsyncFaultCheck: raises (returned -4) if a wave-pair kernel of this thread's
+    async device-mode calls reported a protocol fault since the last check.  Synchronise first."""
+    _check(lib().BRB_CryptoGPU_AsyncFaultCheck(), "BRB_CryptoGPU_AsyncFaultCheck")
 
 
 def test_option(name: str, value: int) -> int:

@@ -104,6 +104,7 @@ namespace brb_api {
 struct Workspaces {
     std::vector<std::pair<void *, size_t>> by_dev;   // (ptr, capacity) per device ordinal
     uint32_t *fault_word = nullptr;                   // pair_fault.h: the thread's fault word
+    uint32_t *async_word = nullptr;                   // ... and its sticky word for ASYNC calls
     void release()
     {
         for (size_t d = 0; d < by_dev.size(); d++)
@@ -112,10 +113,11 @@ struct Workspaces {
                 (void)hipFree(by_dev[d].first);
                 by_dev[d] = {nullptr, 0};
             }
-        if (fault_word) {
-            (void)hipHostFree(fault_word);
-            fault_word = nullptr;
-        }
+        for (uint32_t **w : {&fault_word, &async_word})
+            if (*w) {
+                (void)hipHostFree(*w);
+                *w = nullptr;
+            }
     }
     ~Workspaces() { release(); }
 };
@@ -127,28 +129,33 @@ thread_local uint32_t *t_fault_armed = nullptr;       // the word the pair kerne
 // once the stream has drained).  Allocated on the thread's first armed call; nullptr if it cannot be
 // had.  The word is 0 between calls (check() clears it), so arming a call is one thread-local store
 // and nothing runs between the caller and the launch (the bench's events see no host work).
-uint32_t *fault_word()
+uint32_t *alloc_fault_word(uint32_t **slot)
 {
-    if (!t_ws.fault_word) {
+    if (!*slot) {
         void *p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }
-        t_ws.fault_word = static_cast<uint32_t *>(p);
-        *t_ws.fault_word = 0;
+        *slot = static_cast<uint32_t *>(p);
+        **slot = 0;
     }
-    return t_ws.fault_word;
+    return *slot;
 }
+uint32_t *fault_word() { return alloc_fault_word(&t_ws.fault_word); }
 
 // Arms the thread's fault word for one synchronous call (pair_fault.h); check() after the stream
-// has drained turns a fault into BRB_BATCH_FAULT.  Unarmed for device-mode async calls.
+// has drained turns a fault into BRB_BATCH_FAULT.  A device-mode async call returns before its
+// kernels run: it arms the thread's sticky async word instead, which BRB_CryptoGPU_AsyncFaultCheck
+// reads (and clears) once the caller has synchronised its streams.
 struct PairFault {
     uint32_t *w = nullptr;
     explicit PairFault(unsigned flags)
     {
-        if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC))
+        if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC)) {
+            t_fault_armed = alloc_fault_word(&t_ws.async_word);
             return;
+        }
         w = fault_word();
         t_fault_armed = w;
     }
@@ -208,6 +215,12 @@ namespace brb {
 uint32_t *pair_fault_word()
 {
     return brb_api::t_fault_armed;
+}
+uint32_t *pair_fault_arm(uint32_t *w)
+{
+    uint32_t *prev = brb_api::t_fault_armed;
+    brb_api::t_fault_armed = w;
+    return prev;
 }
 }  // namespace brb
 
@@ -1053,6 +1066,18 @@ void BRB_CryptoGPU_ThreadCleanup(void)
 const char *BRB_CryptoGPU_LastError(void)
 {
     return t_err.c_str();
+}
+
+int BRB_CryptoGPU_AsyncFaultCheck(void)
+{
+    brb_api::clear_err();
+    uint32_t *w = brb_api::t_ws.async_word;
+    if (!w || __atomic_load_n(w, __ATOMIC_ACQUIRE) == 0)
+        return BRB_BATCH_OK;
+    __atomic_store_n(w, 0u, __ATOMIC_RELAXED);
+    set_err("wave-pair protocol fault in a device-mode BRB_BATCH_ASYNC call of this thread since the last check: "
+            "that call's outputs (and RC4 states) are wrong");
+    return BRB_BATCH_FAULT;
 }
 
 const char *BRB_CryptoGPU_Version(void)

@@ -29,8 +29,10 @@ BRB_DEV void seg_lane(brb_md5::FunnelT<RW> &f, const uint8_t *__restrict__ data,
 {
     uint64_t before = 0;
     auto skip_empty = [&](uint64_t kk) {                // the next segment with bytes (an empty one's
-        while (kk < k1 && slen[kk] == 0)                // address need not be memory)
-            kk++;
+        while (kk < k1 && slen[kk] == 0) {              // address need not be memory); a beat per
+            kk++;                                       // skipped segment: a million-long run of empty
+            beat();                                     // ones outlasts the partner's idle budget
+        }
         return kk;
     };
     auto start = [&](brb_io::BlockSrc &src, uint64_t kk, uint64_t pre, uint64_t &len) {

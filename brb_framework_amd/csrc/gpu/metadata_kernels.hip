@@ -86,6 +86,7 @@ BRB_DEV BRB_MetaDataUnpackInfo unpack_lane(brb_md5::FunnelT<RW> &f, const uint8_
         code = BRB_METADATA_UNPACK_SUCCESS;
         uint64_t sz = hd.qw(20);                            // item 0's sz (bytes 80..87)
         for (int32_t i = 0; i < item_count; i++) {          // :202
+            beat();                                         // per item: an empty one runs no block
             remaining = size - offset;                      // :213 (unsigned long)
             if (remaining < kItemStruct) {                  // :216-224
                 needed = kItemStruct - remaining;

@@ -521,6 +521,9 @@ BRB_DEV bool pair_io(const Rc4Mail &m, uint32_t nblk, uint32_t nloop, brb_io::Bl
     return bo >= nloop;
 }
 
+// STALL (both pair kernels): test option pair_stall, as rc4_crypt_pair_kernel -- the first workgroup's
+// first partner wave stages its blocks but never hands one over, so both waves' bounded waits give up.
+template <bool STALL>
 __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *__restrict__ states,
                                                                       const uint8_t *__restrict__ payload,
                                                                       const uint64_t *__restrict__ offs,
@@ -565,6 +568,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
         snk.init(live ? frames + foffs[s] + 32 : nullptr, live && F > 32 ? F - 32 : 0);
         Md5State st = md5_iv();
         const uint64_t nw = 16 * uint64_t(nblk);
+        const bool stalled = STALL && blockIdx.x == 0 && w4 == 0;
         const bool io_ok = pair_io(
             m, nblk, nloop, src,
             [&](const uint32_t (&c)[16], uint32_t b) {
@@ -572,7 +576,8 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
 #pragma unroll
                     for (int i = 0; i < 16; i++)
                         rin[w4][b & 1][i][lane] = c[i];
-                    pc_publish(m.in_cnt, b + 1);
+                    if (!stalled)
+                        pc_publish(m.in_cnt, b + 1);
                     uint32_t w[16];
 #pragma unroll
                     for (int i = 0; i < 16; i++)
@@ -713,6 +718,7 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_frame_pair_kernel(uint8_t *_
     g.store(state);
 }
 
+template <bool STALL>
 __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__restrict__ states, const uint8_t *in,
                                                                      uint8_t *out, const uint64_t *__restrict__ offs,
                                                                      const uint32_t *__restrict__ lens, uint64_t n,
@@ -757,10 +763,11 @@ __global__ __launch_bounds__(2 * kWave) void rc4md5_open_pair_kernel(uint8_t *__
         Md5State st = md5_iv();
         const uint64_t nw = 16 * uint64_t(nmd);
         uint32_t cur[16], h[6] = {0, 0, 0, 0, 0, 0};
+        const bool stalled = STALL && blockIdx.x == 0 && w4 == 0;
         const bool io_ok = pair_io(
             m, nfb, nloop, src,
             [&](const uint32_t (&c)[16], uint32_t b) {
-                if (b < nfb) {
+                if (b < nfb && !stalled) {
 #pragma unroll
                     for (int i = 0; i < 16; i++)
                         rin[w4][b & 1][i][lane] = c[i];
@@ -892,10 +899,14 @@ hipError_t launch_rc4md5_frame(uint8_t *states, const uint8_t *payload, const ui
 {
     if (n == 0)
         return hipSuccess;
-    if (brb_opt::get(brb_opt::kRc4Pair) != 0)
-        rc4md5_frame_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n,
-                                                                   sidx, brb::pair_fault_word());
-    else
+    if (brb_opt::get(brb_opt::kRc4Pair) != 0) {
+        if (brb_opt::get(brb_opt::kPairStall) != 0)
+            rc4md5_frame_pair_kernel<true><<<grid_for(n), 2 * kWave, 0, s>>>(states, payload, offs, lens, salts, frames,
+                                                                             foffs, n, sidx, brb::pair_fault_word());
+        else
+            rc4md5_frame_pair_kernel<false><<<grid_for(n), 2 * kWave, 0, s>>>(states, payload, offs, lens, salts, frames,
+                                                                              foffs, n, sidx, brb::pair_fault_word());
+    } else
         rc4md5_frame_kernel<<<grid_for(n), kWave, 0, s>>>(states, payload, offs, lens, salts, frames, foffs, n, sidx);
     return hipGetLastError();
 }
@@ -906,10 +917,14 @@ hipError_t launch_rc4md5_open(uint8_t *states, const uint8_t *in, uint8_t *out, 
 {
     if (n == 0)
         return hipSuccess;
-    if (brb_opt::get(brb_opt::kRc4Pair) != 0)
-        rc4md5_open_pair_kernel<<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs,
-                                                                  brb::pair_fault_word());
-    else
+    if (brb_opt::get(brb_opt::kRc4Pair) != 0) {
+        if (brb_opt::get(brb_opt::kPairStall) != 0)
+            rc4md5_open_pair_kernel<true><<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx,
+                                                                            ooffs, brb::pair_fault_word());
+        else
+            rc4md5_open_pair_kernel<false><<<grid_for(n), 2 * kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx,
+                                                                             ooffs, brb::pair_fault_word());
+    } else
         rc4md5_open_kernel<<<grid_for(n), kWave, 0, s>>>(states, in, out, offs, lens, n, valid, sidx, ooffs);
     return hipGetLastError();
 }

@@ -174,6 +174,9 @@ struct Round {
     std::vector<size_t> group_valid;       // group -> offset of its valid flags in h_meta
     hipEvent_t done = nullptr;
     hipEvent_t ev_h2d = nullptr, ev_kern = nullptr;   // pipelined: inputs landed, kernels finished
+    // pair_fault.h: the round's fault word (page-locked, mapped), armed around its kernel launches and
+    // read once the round is done; cleared before every launch of the round
+    uint32_t *fault = nullptr;
     bool in_flight = false;
 
     void release()
@@ -184,6 +187,7 @@ struct Round {
         (void)hipHostFree(h_in);
         (void)hipHostFree(h_out);
         (void)hipHostFree(h_meta);
+        (void)hipHostFree(fault);
         for (hipEvent_t ev : {done, ev_h2d, ev_kern})
             if (ev)
                 (void)hipEventDestroy(ev);
@@ -253,7 +257,7 @@ struct BRB_TransformBatcher {
     hipError_t alloc_round(Round &x)
     {
         hipError_t e;
-        void *od = nullptr, *md = nullptr;
+        void *od = nullptr, *md = nullptr, *fw = nullptr;
         if ((e = hipMalloc(&x.d_in, up(cap, kAlign))) != hipSuccess || (e = hipMalloc(&x.d_out, out_cap)) != hipSuccess ||
             (e = hipMalloc(&x.d_meta, meta_cap)) != hipSuccess ||
             (e = hipHostMalloc(&x.h_in, up(cap, kAlign), hipHostMallocDefault)) != hipSuccess ||
@@ -261,10 +265,13 @@ struct BRB_TransformBatcher {
             (e = hipHostMalloc(&x.h_meta, meta_cap, hipHostMallocDefault)) != hipSuccess ||
             (e = hipHostGetDevicePointer(&od, x.h_out, 0)) != hipSuccess ||
             (e = hipHostGetDevicePointer(&md, x.h_meta, 0)) != hipSuccess ||
+            (e = hipHostMalloc(&fw, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&x.ev_h2d, hipEventDisableTiming)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&x.ev_kern, hipEventDisableTiming)) != hipSuccess)
             return e;
+        x.fault = static_cast<uint32_t *>(fw);
+        __atomic_store_n(x.fault, 0u, __ATOMIC_RELAXED);
         x.out_dev = reinterpret_cast<uintptr_t>(od);
         x.meta_dev = reinterpret_cast<uintptr_t>(md);
         x.slots.resize(max_items);
@@ -558,6 +565,14 @@ static int enqueue_round(BRB_TransformBatcher *b, Round &R, bool *started)
         return fail_hip("hipMemcpyAsync H2D", e);
     if (split && ((e = hipEventRecord(R.ev_h2d, sh)) != hipSuccess || (e = hipStreamWaitEvent(s, R.ev_h2d, 0)) != hipSuccess))
         return fail_hip("H2D event", e);
+    // the round's pair kernels report a protocol fault into R.fault (pair_fault.h); the word's last
+    // reader was this round's previous delivery, so no kernel still writes it
+    __atomic_store_n(R.fault, 0u, __ATOMIC_RELAXED);
+    struct Arm {
+        uint32_t *prev;
+        explicit Arm(uint32_t *w) : prev(brb::pair_fault_arm(w)) {}
+        ~Arm() { brb::pair_fault_arm(prev); }
+    } arm(R.fault);
     uint8_t *zbase = reinterpret_cast<uint8_t *>(R.out_dev);   // zero-copy: inputs and outputs
     uint8_t *zvalid = reinterpret_cast<uint8_t *>(R.meta_dev);
     size_t vpos = o_valid;
@@ -652,6 +667,16 @@ static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDon
         fail_hip("round completion", e);
         const std::string why = brb_api::t_err;
         set_err("%s; round of %zu buffers dropped", why.c_str(), R.items.size());
+        drop_round(R, done, user);
+        return -1;
+    }
+    if (__atomic_load_n(R.fault, __ATOMIC_ACQUIRE) != 0) {
+        // a pair kernel's bounded wait gave up: its outputs, valid flags and the RC4 states it
+        // advanced are wrong, so nothing of the round is delivered as data (the reference's only
+        // integrity check, ev_kq_aio_transform.c:157-184, must never pass over wrong bytes)
+        set_err("wave-pair protocol fault: a kernel of the round gave up waiting on its partner wave; round of %zu "
+                "buffers dropped (its connections' states are out of step: re-key them with Enable)",
+                R.items.size());
         drop_round(R, done, user);
         return -1;
     }
@@ -782,18 +807,22 @@ static int64_t flush_all(BRB_TransformBatcher *b, BRB_TransformDone done, void *
         dropped |= p.dropped;
         failed += p.failed ? 1u : 0u;
     }
-    if (dropped)
-        return BRB_BATCH_DROPPED;
     if (failed) {
         // parts that could not select their device keep their rounds pending, while the
         // other parts' buffers were delivered (callbacks fired, states advanced): say so instead of
-        // returning "not done" for the whole call
+        // returning "not done" for the whole call.  ADVICE r04: a round of another part dropped in the
+        // same call is reported with it, not instead of it -- DROPPED tells the caller that nothing is
+        // pending, and the pending parts' rounds still read their zero-copy inputs in place.
         const std::string why = brb_api::t_err;
         set_err("%u of %u parts could not select their device (%s); their rounds stay pending, %lld buffers of "
-                "the other parts were delivered; Flush again",
-                failed, G, why.c_str(), (long long)total);
-        return total ? BRB_BATCH_PARTIAL : BRB_BATCH_NOT_DONE;
+                "the other parts were delivered%s; Flush again",
+                failed, G, why.c_str(), (long long)total,
+                dropped ? " and a round of another part was dropped (its buffers came back as BRB_TRANSFORM_DROPPED)"
+                        : "");
+        return total || dropped ? BRB_BATCH_PARTIAL : BRB_BATCH_NOT_DONE;
     }
+    if (dropped)
+        return BRB_BATCH_DROPPED;
     return total;
 }
 

@@ -116,17 +116,21 @@ void BRB_RC4_Crypt(BRB_RC4_State *state, const unsigned char *inbuf, unsigned ch
 #define BRB_BATCH_FAULT    (-4)   /* segment digests, MetaData unpack, RC4 pass, RC4+MD5 frame /
                                      open: a wave-pair kernel's bounded wait on its partner wave
                                      gave up (a protocol fault; never a hang).  The call's outputs,
-                                     and for RC4 the states, are wrong.  Reported by synchronous
-                                     calls only (not device-mode BRB_BATCH_ASYNC, not the
-                                     transform batcher's rounds).  Test option pair_stall injects
-                                     one.                                                        */
+                                     and for RC4 the states, are wrong.  Returned by synchronous
+                                     calls; a device-mode BRB_BATCH_ASYNC call cannot know yet and
+                                     returns 1: BRB_CryptoGPU_AsyncFaultCheck() reports it after the
+                                     caller has synchronised its stream.  A transform batcher round
+                                     with a fault is dropped (Flush returns BRB_BATCH_DROPPED).
+                                     Test option pair_stall injects one.                         */
 
 /* flags */
 #define BRB_BATCH_HOST      0x0u   /* pointers are host memory: copied in and out by the call      */
 #define BRB_BATCH_DEVICE    0x1u   /* every pointer (data, offsets, lengths, digests, ctx, words)
                                       is device memory (HBM-resident); nothing crosses PCIe       */
 #define BRB_BATCH_ASYNC     0x2u   /* with BRB_BATCH_DEVICE: enqueue on `hip_stream` and return
-                                      without waiting; the caller synchronises the stream         */
+                                      without waiting; the caller synchronises the stream and then
+                                      calls BRB_CryptoGPU_AsyncFaultCheck() (same thread) before it
+                                      trusts the outputs of wave-pair calls (BRB_BATCH_FAULT)     */
 #define BRB_BATCH_ALL_DEVICES 0x4u /* host mode only (every batch call except MemBuffer):
                                       split the records (blocks, streams, packs) into contiguous
                                       ranges [g*n/G, (g+1)*n/G), one per visible device g < G, run
@@ -309,7 +313,9 @@ int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void
  * buffers still gets its callback, in order, with valid = BRB_TRANSFORM_DROPPED, out = NULL and
  * out_len = 0, and the call returns BRB_BATCH_DROPPED (-2) with the reason in LastError -- also when
  * another round was delivered in the same call, whose buffers came back through their callbacks as
- * usual.  Such connections are out of step with their peers, as after a lost buffer in the
+ * usual (and BRB_BATCH_PARTIAL when, besides, a part's round stays pending).  A round in which a
+ * wave-pair kernel reports a protocol fault (BRB_BATCH_FAULT above) is dropped the same way, so no
+ * output, frame or valid flag computed over wrong bytes is ever delivered.  Such connections are out of step with their peers, as after a lost buffer in the
  * reference, and are re-keyed with Enable.  On a pipelined batcher Flush first delivers the round
  * FlushAsync left running, so Flush drains everything.  A batcher's calls run on the device it was
  * created on and leave the calling thread's current device unchanged. */
@@ -381,6 +387,11 @@ int BRB_CryptoGPU_GetDevice(void);
 void BRB_CryptoGPU_ThreadCleanup(void);
 /* Last error of the calling thread ("" if none). */
 const char *BRB_CryptoGPU_LastError(void);
+/* Wave-pair faults of the calling thread's device-mode BRB_BATCH_ASYNC calls: 1 if none of the
+ * wave-pair kernels they enqueued since the last check reported a protocol fault, BRB_BATCH_FAULT
+ * (-4) if one did (reason in LastError; the report is cleared).  Call it after synchronising the
+ * streams those calls used: a kernel still running has not reported yet. */
+int BRB_CryptoGPU_AsyncFaultCheck(void);
 /* Page-lock [p, p + len) for the GPU (hipHostRegister, mapped) so that zero-copy batchers can read
  * it: 1 = done, 0 = no device / HIP error (LastError), -1 = bad arguments.  Unregister takes the
  * same `p`. */
@@ -401,8 +412,9 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * "line_slots" 0/2/3 (LDS-DMA ring slots of the line-staged segment and MetaData kernels: each
  * kernel's default, or forced), "rc4md5_pair" 1/0 (BRB_RC4MD5_FrameBatch / OpenBatch on keystream +
  * partner wave pairs / one wave per connection), "rc4_pair" 1/0 (BRB_RC4_CryptBatch likewise; a forced
- * "rc4_sector" value selects the one-wave kernel), "pair_stall" 0/1 (1: the segment, MetaData and RC4
- * pass wave pairs get a protocol fault injected, so the call returns BRB_BATCH_FAULT).  Returns 1 and the previous
+ * "rc4_sector" value selects the one-wave kernel), "pair_stall" 0/1 (1: the segment, MetaData, RC4
+ * pass and RC4+MD5 frame / open wave pairs get a protocol fault injected, so the call returns
+ * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

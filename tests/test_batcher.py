@@ -320,3 +320,66 @@ def test_states_survive_busy_default_stream(brb, orc, torch_dev):
     torch.cuda.synchronize()                       # the default stream's work has all landed
     assert b.state(0, 0) == st and b.state(0, 1) == orc.rc4_init(key)
     b.close()
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+@pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("algo", [1, 2])
+def test_pair_fault_round_dropped(brb, orc, torch_dev, algo, zero_copy, pipelined):
+    """A wave-pair protocol fault inside a batcher round (test option pair_stall, on the pair kernels
+    the rounds run: the RC4 pass, the RC4+MD5 frame and open) drops the round: every buffer comes
+    back with valid = BRB_TRANSFORM_DROPPED and no output, Flush returns BRB_BATCH_DROPPED -- no
+    plaintext, frame or valid flag computed over wrong bytes is delivered (ev_kq_aio_transform.c:
+    157-184 must never pass over them).  After re-keying (Enable) the next round equals the oracle."""
+    rng = np.random.default_rng(100 + algo)
+    C = 96                                        # > 64: the stalled wave's group and ordinary ones
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(C)]
+    b = brb.TransformBatcher(C, 4 << 20, algo, zero_copy=zero_copy, pipelined=pipelined)
+
+    def rekey():
+        for c in range(C):
+            b.enable(c, keys[c])
+        return ([orc.rc4_init(k) for k in keys], [orc.rc4_init(k) for k in keys], [orc.rc4_init(k) for k in keys])
+
+    def submit(rnd, ours_r, ours_w, peer_w):
+        expect = []
+        for c in range(C):
+            n = int(rng.choice([0, 17, 700, 1500, 3000]))
+            payload = workload.gen_records(0x5EED00F6 + rnd, c, 1, n).tobytes() if n else b""
+            if algo == 2:
+                peer_w[c], frame = orc.rc4md5_frame(peer_w[c], payload, c)
+                ours_r[c], dec, ok = orc.rc4md5_open(ours_r[c], frame)
+                expect.append((c, 0, dec, ok))
+                assert b.read(c, frame) == 1
+                ours_w[c], out = orc.rc4md5_frame(ours_w[c], payload, rnd + c)
+            else:
+                peer_w[c], wire = orc.rc4_crypt(peer_w[c], payload)
+                ours_r[c], dec = orc.rc4_crypt(ours_r[c], wire)
+                expect.append((c, 0, dec, 1))
+                assert b.read(c, wire) == 1
+                ours_w[c], out = orc.rc4_crypt(ours_w[c], payload)
+            expect.append((c, 1, out, 1))
+            assert b.write(c, payload, rnd + c) == 1
+        return expect
+
+    ours_r, ours_w, peer_w = rekey()
+    expect = submit(0, ours_r, ours_w, peer_w)
+    dropped = [(c, op, b"", brb.TRANSFORM_DROPPED) for c, op, _, _ in expect]
+    with brb.TestOption("rc4_pair", 1), brb.TestOption("rc4md5_pair", 1), brb.TestOption("pair_stall", 1):
+        if pipelined:
+            assert b.flush_async() == []          # launched with the stalled kernels, not delivered
+        else:
+            with pytest.raises(RuntimeError, match="wave-pair protocol fault.*dropped") as ei:
+                b.flush()
+    if pipelined:
+        with pytest.raises(RuntimeError, match="wave-pair protocol fault.*dropped") as ei:
+            b.flush()
+    assert ei.value.code == brb.BATCH_DROPPED
+    assert ei.value.results == dropped
+    assert b.flush() == []                        # the dropped round is gone, nothing re-runs
+    ours_r, ours_w, peer_w = rekey()              # its connections are re-keyed, as after a lost buffer
+    expect = submit(1, ours_r, ours_w, peer_w)
+    _check_round(b.flush(), expect, 1)
+    for c in range(0, C, 5):
+        assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
+    b.close()

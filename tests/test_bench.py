@@ -85,3 +85,92 @@ def test_timed_steps_multi_stream_brackets_all():
     clock.log.clear()
     _, per1 = bench.timed_steps(launch, 1, ["s0"], lambda: None, lambda x: x, torch)
     assert clock.log == ["event", "launch0", "event"] and abs(per1 - 2.0e-3) < 1e-12
+
+
+# ---- roofline.traffic / roofline.compute come only from a PMC pass of the timed kernels ------------
+ROCPROF_NAMES = {
+    "cfg2_md5": ["void brb_digest::digest_line_kernel<(anonymous namespace)::Md5Alg, 8, true, true, true>"
+                 "(unsigned char const*, unsigned int, unsigned long, unsigned char*)"],
+    "cfg4_blowfish": ["void brb_bf::bf_rep_kernel<2, false>(unsigned long const*, unsigned long*, unsigned long)",
+                      "void brb_bf::bf_rep_kernel<2, true>(unsigned long const*, unsigned long*, unsigned long)"],
+    "f1_rc4": ["void (anonymous namespace)::rc4_crypt_pair_kernel<false>(unsigned char*, unsigned char const*, "
+               "unsigned char*, unsigned long const*, unsigned int const*, unsigned long, ...)"],
+    "f1_rc4md5": ["void (anonymous namespace)::rc4md5_frame_pair_kernel<false>(unsigned char*, ...)",
+                  "void (anonymous namespace)::rc4md5_open_pair_kernel<false>(unsigned char*, ...)"],
+    "f4_metadata": ["void (anonymous namespace)::metadata_line_kernel<4, 2, true, false>(unsigned char const*, ...)"],
+    "f4_md5seg": ["void (anonymous namespace)::md5_seg_pc_kernel<4, false>(unsigned char const*, ...)"],
+}
+
+
+def _lib_opt():
+    from brb_framework_amd import crypto
+
+    def opt(name):
+        old = crypto.test_option(name, 0)
+        crypto.test_option(name, old)
+        return old
+    return opt
+
+
+def test_kernel_id_and_default_selection():
+    """kernel_id strips namespaces and arguments; under the library's default test options the timed
+    kernels of each line are the product kernels (the wave pairs for RC4, frames, MetaData, segments)."""
+    opt = _lib_opt()
+    assert bench.kernel_id(ROCPROF_NAMES["cfg2_md5"][0]) == "digest_line_kernel<Md5Alg, 8, true, true, true>"
+    assert bench.kernel_id("(anonymous namespace)::rc4md5_open_pair_kernel(unsigned char*, ...") == \
+        "rc4md5_open_pair_kernel"
+    for key, names in ROCPROF_NAMES.items():
+        ids = sorted(bench.kernel_id(n) for n in names)
+        assert bench.kernels_match(ids, bench.timed_kernel_patterns(key, opt)), (key, ids)
+    # the pre-pair RC4 kernel (round 4's stale f1 evidence) does not pass for the pair line
+    assert not bench.kernels_match(["rc4_crypt_kernel<true>"], bench.timed_kernel_patterns("f1_rc4", opt))
+    # one-to-one: a missing or an extra kernel fails
+    assert not bench.kernels_match(["rc4md5_frame_pair_kernel<false>"], bench.timed_kernel_patterns("f1_rc4md5", opt))
+    assert not bench.kernels_match([], bench.timed_kernel_patterns("cfg2_md5", opt))
+
+
+def test_load_pmc_refuses_other_kernels(tmp_path):
+    """A PMC entry of another kernel (or one that does not name its kernels) gives no traffic and a
+    refused compute block, never numbers; the matching entry is used."""
+    opt = _lib_opt()
+    det = {"source": "x.txt", "sq_insts_valu": 2.8e7, "sq_waves": 2048.0, "sq_insts_lds": 1e7}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"f1_rc4": 1000, "f1_rc4_detail": dict(det, kernels=["rc4_crypt_kernel<true>"]),
+                             "f4_md5seg": 10, "f4_md5seg_detail": det}))
+    old = bench.OPT
+    bench.OPT = opt
+    try:
+        for key in ("f1_rc4", "f4_md5seg"):
+            t = bench.traffic_fields(str(p), key)
+            assert t["traffic"] is None and "not used" in t["traffic_source"]
+            c = bench.issue_compute(str(p), key, 1e-4)
+            assert set(c) == {"refused"}
+        p.write_text(json.dumps({"f1_rc4": 1000, "f1_rc4_detail": dict(det, kernels=["rc4_crypt_pair_kernel<false>"])}))
+        assert bench.traffic_fields(str(p), "f1_rc4")["traffic"] == 1000
+        c = bench.issue_compute(str(p), "f1_rc4", 1e-4)
+        assert c["kernels"] == ["rc4_crypt_pair_kernel<false>"] and c["waves_per_simd"] == 2.0
+    finally:
+        bench.OPT = old
+
+
+def test_committed_evidence_compute_matches_timed_kernels():
+    """Every line of the newest committed evidence (profiles/r*_evidence/lines.json written with
+    kernel identities) carries roofline.compute from the kernels its timed region launched."""
+    import glob
+    dirs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_evidence", "lines.json")))
+    checked = 0
+    for path in reversed(dirs):
+        lines = json.load(open(path))
+        if not any("timed_kernel_ids" in (e.get("timed_region") or {}) for e in lines.values()):
+            continue                          # written before the check existed
+        for name, e in lines.items():
+            t = e.get("timed_region") or {}
+            comp = (e["line"].get("roofline") or {}).get("compute")
+            if comp and t:
+                assert t.get("compute_kernels_match") is True, (path, name, t.get("compute_kernels"),
+                                                               t.get("timed_kernel_ids"))
+                checked += 1
+        break
+    if dirs and checked == 0:
+        import pytest
+        pytest.skip("no committed evidence with kernel identities yet")

@@ -307,22 +307,26 @@ def test_unpack_large_items(brb, orc, seg_line):
 @pytest.mark.parametrize("seg_line", [1, 2])
 def test_unpack_long_stretches(brb, orc, seg_line):
     """Work that outlasts a wait without progress: (1) a pack of 300 000 empty items (8 MB, tens of
-    thousands of lines in which the walk emits no message word) beside ordinary packs, and (2) a
-    64 MiB item in a pack placed more than 2 GiB from its group's other packs (the per-lane path,
-    the producer alone while its partner waits for the next plan).  Every field vs the oracle."""
+    thousands of lines in which the walk emits no message word) beside ordinary packs, (2) a 64 MiB
+    item in a pack placed more than 2 GiB from its group's other packs (the per-lane path, the
+    producer alone while its partner waits for the next plan), and (3) the empty-item pack again on
+    that per-lane path, where an empty item runs no block (the walk beats once per item).
+    Every field vs the oracle."""
     import torch
     rng = np.random.default_rng(23)
     empty = build([(i & 0xFF, 1, b"") for i in range(300_000)])
     small = [build([(1, 2, rng.integers(0, 256, 300, dtype=np.uint8).tobytes())]) for _ in range(70)]
     huge = build([(3, 4, rng.integers(0, 256, 64 << 20, dtype=np.uint8).tobytes())])
-    packs = [empty] + small[:63] + [huge] + small[63:]
+    packs = [empty] + small[:63] + [huge, empty] + small[63:]
     far = (1 << 31) + 12345
-    total = far + len(huge) + 64
+    total = far + len(huge) + 8 + len(empty) + 64
     d = torch.zeros(total, dtype=torch.uint8, device="cuda")
     offs, pos = [], 0
     for i, p in enumerate(packs):
-        if p is huge:
+        if i == 64:
             o = far
+        elif i == 65:
+            o = far + len(huge) + 8
         else:
             o = pos
             pos += len(p) + 3
@@ -338,6 +342,7 @@ def test_unpack_long_stretches(brb, orc, seg_line):
     want = [orc.metadata_unpack(p) for p in packs]
     assert infos_as_tuples(dev) == want
     assert want[64][0] == 7                                # the 64 MiB item unpacks (METADATA_UNPACK_SUCCESS)
+    assert want[65] == want[0]
     assert want[0][1] == 299_999                           # every empty item walked; the last one is the
     #                                                        reference's < 32-bytes-left quirk (NEED_MORE_DATA_METAITEM)
     del d

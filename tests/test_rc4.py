@@ -599,3 +599,66 @@ def test_rc4_pair_fault_reported(brb, orc, torch_dev):
     brb.rc4_crypt_batch(st, out, offs, lens)
     want_st, want = _oracle_crypt(orc, states, data, offs, lens)
     assert np.array_equal(out, want) and np.array_equal(st, want_st)
+
+
+@pytest.mark.gpu
+def test_rc4md5_pair_fault_reported(brb, orc, torch_dev):
+    """A protocol fault in the RC4+MD5 frame / open wave pairs (test option pair_stall: the first
+    partner wave stages its blocks but never hands one over) is reported as BRB_BATCH_FAULT (-4) by
+    FrameBatch and OpenBatch in host and device mode; the next calls on the thread are exact."""
+    torch = torch_dev
+    n = 128
+    offs, lens, total = _layout([1500] * (n - 2) + [0, 200])
+    payload = workload.gen_records(SEED + 10, 0, 1, total + 4)
+    foffs, _, ftotal = _layout([30 + int(x) for x in lens])
+    salts = np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15 & 0xFFFFFFFF)
+    states = brb.rc4_states(_keys(n, 41))
+    frames0 = np.zeros(ftotal + 8, np.uint8)
+    want_st, want_fr = _oracle_frames(orc, states, payload, offs, lens, salts, frames0, foffs)
+    flens = (lens + 30).astype(np.uint32)
+    with brb.TestOption("rc4md5_pair", 1), brb.TestOption("pair_stall", 1):
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4md5_frame_batch(states.copy(), payload, offs, lens, salts, frames0.copy(), foffs)
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4md5_frame_batch(_to(torch, states), _to(torch, payload), _to(torch, offs), _to(torch, lens),
+                                   _to(torch, salts), _to(torch, frames0), _to(torch, foffs))
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4md5_open_batch(states.copy(), want_fr.copy(), foffs, flens)
+        with pytest.raises(RuntimeError, match=r"returned -4: wave-pair protocol fault"):
+            brb.rc4md5_open_batch(_to(torch, states), _to(torch, want_fr), _to(torch, foffs), _to(torch, flens))
+    hs, hf = states.copy(), frames0.copy()
+    brb.rc4md5_frame_batch(hs, payload, offs, lens, salts, hf, foffs)
+    assert np.array_equal(hf, want_fr) and np.array_equal(hs, want_st)
+    os_, buf = states.copy(), want_fr.copy()
+    _, valid = brb.rc4md5_open_batch(os_, buf, foffs, flens)
+    assert valid.tolist() == [1] * n and np.array_equal(os_, want_st)
+    for i in range(n):
+        o, m = int(foffs[i]), int(lens[i])
+        assert buf[o + 30:o + 30 + m].tobytes() == payload[int(offs[i]):int(offs[i]) + m].tobytes(), i
+
+
+@pytest.mark.gpu
+def test_async_pair_fault_check(brb, orc, torch_dev):
+    """Device-mode BRB_BATCH_ASYNC calls return before their kernels run, so a wave-pair fault
+    (pair_stall) cannot be their return code: BRB_CryptoGPU_AsyncFaultCheck() reports it once the
+    caller has synchronised (-4, then cleared), and stays clean after a clean async call."""
+    torch = torch_dev
+    n = 128
+    offs, lens, total = _layout([4096] * n)
+    data = workload.gen_records(SEED + 11, 0, 1, total)
+    states = brb.rc4_states(_keys(n, 43))
+    brb.async_fault_check()                                  # nothing pending on this thread
+    args = (_to(torch, offs), _to(torch, lens))
+    with brb.TestOption("rc4_pair", 1), brb.TestOption("pair_stall", 1):
+        brb.rc4_crypt_batch(_to(torch, states), _to(torch, data), *args, async_=True)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match=r"AsyncFaultCheck returned -4: wave-pair protocol fault"):
+        brb.async_fault_check()
+    brb.async_fault_check()                                  # the report was cleared
+    ts, td = _to(torch, states), _to(torch, data)
+    with brb.TestOption("rc4_pair", 1):
+        brb.rc4_crypt_batch(ts, td, *args, async_=True)
+    torch.cuda.synchronize()
+    brb.async_fault_check()
+    want_st, want = _oracle_crypt(orc, states, data, offs, lens)
+    assert np.array_equal(td.cpu().numpy(), want) and np.array_equal(ts.cpu().numpy(), want_st)

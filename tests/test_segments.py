@@ -214,6 +214,36 @@ def test_segments_long_lane_in_wide_group(brb, torch_dev, seg_line):
     t.cuda.empty_cache()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("seg_line", [1, 2])
+def test_segments_long_empty_run_per_lane(brb, torch_dev, seg_line):
+    """A record of 1.5 million empty segments and then one with bytes: its group holds more segments
+    than the wave's table, so it takes the per-lane path (in the wave-pair kernel the producer alone,
+    its partner waiting).  Skipping the empty run emits no block, and outlasts a wait without progress
+    unless the walk beats per skipped segment.  128 records vs hashlib."""
+    t = torch_dev
+    rng = np.random.default_rng(53)
+    pool = workload.gen_records(0x5EED00FC, 0, 1, 1 << 20)
+    E, n = 1_500_000, 128
+    counts = np.array([E + 1] + [2] * (n - 1), np.uint64)
+    first = np.zeros(n + 1, np.uint64)
+    first[1:] = np.cumsum(counts)
+    nseg = int(first[-1])
+    lens = np.zeros(nseg, np.uint32)
+    offs = np.zeros(nseg, np.uint64)
+    lens[E] = 100
+    offs[E] = 4097
+    lens[E + 1:] = rng.integers(1, 1200, nseg - E - 1).astype(np.uint32)
+    offs[E + 1:] = rng.integers(0, (1 << 20) - 1200, nseg - E - 1).astype(np.uint64)
+    dev = lambda a: t.from_numpy(np.ascontiguousarray(a)).cuda()   # noqa: E731
+    with brb.TestOption("seg_line", seg_line):
+        got = brb.md5_batch_segments(dev(pool), dev(offs), dev(lens), dev(first)).cpu().numpy()
+    for i in range(n):
+        msg = b"".join(pool[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+                       for k in range(max(int(first[i]), E), int(first[i + 1])))
+        assert got[i].tobytes() == hashlib.md5(msg).digest(), i
+
+
 def test_segments_equal_streaming_oracle(brb, orc):
     """The oracle's BRB_MD5Init/UpdateBig/Final restatement over the items = the batch digest."""
     import ctypes

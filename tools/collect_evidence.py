@@ -35,6 +35,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_id  # noqa: E402  (stdlib-only at import)
 PEAK = 8000.0
 SENTINEL = "spin_kernel"
 
@@ -123,6 +125,16 @@ def main():
             regs = regions(dispatches(traces[0]))
             chk = line_check(line, regs)
             entry["timed_region"] = chk
+            comp = (line.get("roofline") or {}).get("compute") or {}
+            if chk and comp:
+                # the line's compute / traffic must come from a PMC pass of the kernels it timed
+                timed = sorted(kernel_id(k) for k in chk["kernels"])
+                chk["timed_kernel_ids"] = timed
+                chk["compute_kernels"] = comp.get("kernels")
+                chk["compute_kernels_match"] = comp.get("kernels") == timed
+                if not chk["compute_kernels_match"]:
+                    print(f"WARNING {name}: roofline.compute from {comp.get('kernels')} "
+                          f"({comp.get('refused') or comp.get('source')}), timed {timed}", file=sys.stderr)
             if "cfg5" in line:
                 sub = dict(line["cfg5"])
                 sub["roofline"] = {"launch_us_avg": sub.get("launch_us_avg"),

@@ -19,6 +19,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_id  # noqa: E402  (stdlib-only at import)
 
 
 def pmc_means(d, pat):
@@ -28,6 +30,17 @@ def pmc_means(d, pat):
             if pat in row["Kernel_Name"]:
                 acc.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def pmc_kernels(d, pat):
+    """The distinct kernels (bench.kernel_id) the passes profiled under filter `pat`: bench.py uses
+    an entry only for a line whose timed region launches exactly these."""
+    ks = set()
+    for p in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+        for row in csv.DictReader(open(p)):
+            if pat in row["Kernel_Name"]:
+                ks.add(kernel_id(row["Kernel_Name"]))
+    return sorted(ks)
 
 
 def timed_region(trace_csv, pat, bench_json):
@@ -126,8 +139,10 @@ def main():
             continue
         summ = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), d, pat],
                               capture_output=True, text=True).stdout
+        kern = pmc_kernels(d, pat)
         with open(os.path.join(prof, f"{tag}_pmc_{key}.txt"), "w") as f:
             f.write(f"# rocprofv3 --pmc passes (tools/gpu_pmc.sh), kernel filter '{pat}', mean per dispatch\n")
+            f.write(f"# kernels: {kern}\n")
             f.write(summ)
         m = pmc_means(d, pat)
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
@@ -135,7 +150,7 @@ def main():
             write = m["WRITE_SIZE"] * 1024 * per
             traffic[key] = int(fetch + write)
             traffic[key + "_detail"] = {"fetch_bytes": int(fetch), "write_bytes": int(write),
-                                        "source": f"profiles/{tag}_pmc_{key}.txt",
+                                        "source": f"profiles/{tag}_pmc_{key}.txt", "kernels": kern,
                                         "formula": "(FETCH_SIZE*2 + WRITE_SIZE) * 1024 per dispatch"
                                                    + (f" x {per} dispatches per step" if per > 1 else ""),
                                         **counters(m)}
