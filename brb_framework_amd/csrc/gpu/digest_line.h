@@ -24,7 +24,11 @@
 // data[r * rec_len .. (r + 1) * rec_len).
 #pragma once
 
+#include <atomic>
+#include <mutex>
+
 #include "dma_stage.h"
+#include "test_options.h"
 
 // Diagnostic hooks (tools/mb/line_probe.hip defines them; empty in the product build).
 #ifndef BRB_LINE_PROBE
@@ -81,34 +85,127 @@ BRB_DEV void tail_masks(uint32_t t, uint32_t (&tm)[16], uint32_t (&tp)[16])
 // (1 Mi x 1500 B, tools/mb/line_probe.hip); with tickets the faster wave simply takes more groups.
 // launch_bounds: two waves per SIMD (4-wave workgroups: two per CU, 64 KiB of LDS each; 8-wave
 // workgroups: one per CU, 128 KiB).
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool NT = false, bool DYN = false>
+//
+// POOL (with DYN; round 5): the tail of the batch is balanced across the chip.
+// A workgroup's LDS tickets cover only its first `t_own` rounds of groups (b + t G, t < t_own); the
+// groups after them form a pool split over kPoolHeads heads in HBM (pool_head), head h holding pool
+// groups h, h + 8, ...  A wave whose workgroup has no ticket left takes pool groups from the head
+// of its own XCD (HW_REG_XCC_ID) and, once that one is empty, sweeps the other heads (an LDS mask
+// of heads the workgroup found empty saves the repeat).  Why: the workgroups of a static split end
+// between 257 and 291 us (1 Mi x 1500 B, profiles/r03/line_probe_cfg5.txt), the odd XCDs 5-13 us
+// behind the even ones, while the kernel is issue-bound: a CU that is done early idles its SIMDs.
+// Round 3's pool (one head, one device-scope atomic per group, its return waited on with the first
+// line pair) cost 3-22 us; here the first pool ticket of a group is requested right after iteration
+// 1's refill, so its return lands while blocks 0-1 are hashed, and 8 heads spread the atomics.
+// The heads of a launch are zeroed by its last workgroup (one device-scope count per workgroup), so
+// the next launch given the same slot (launch_fixed_line: a ring of kPoolSlots per device) starts
+// from zero.
+constexpr uint32_t kPoolHeads = 8;
+constexpr uint32_t kPoolStride = 64;                           // u32: heads 256 B apart
+constexpr uint32_t kPoolSlotWords = (kPoolHeads + 1) * kPoolStride;   // the heads, then the done count
+constexpr uint32_t kPoolSlots = 512;
+
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool NT = false, bool DYN = false, bool POOL = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data,
                                                                              uint32_t rec_len, uint64_t n_rec,
-                                                                             uint8_t *__restrict__ out)
+                                                                             uint8_t *__restrict__ out,
+                                                                             uint32_t *__restrict__ pool,
+                                                                             uint32_t t_own)
 {
     constexpr uint32_t SLOT = 8192;                            // 64 rows x one 128-byte line
     __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
     __shared__ uint32_t next_ticket;
+    __shared__ uint32_t pool_empty, waves_done;                // POOL: heads found empty; waves finished
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t n_groups = (n_rec + 63) / 64;
     const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
     const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
     if (DYN) {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             next_ticket = WAVES;                               // tickets 0 .. WAVES-1: one per wave
+            pool_empty = 0;
+            waves_done = 0;
+        }
         __syncthreads();
     }
+    // POOL: groups [own_end, n_groups) are pooled; pool group p = own_end + p, head p % 8.
+    const uint64_t own_end = POOL ? uint64_t(t_own) * gridDim.x : n_groups;
+    const uint64_t pool_n = POOL && own_end < n_groups ? n_groups - own_end : 0;
+    uint32_t home = 0;
+    if (POOL)
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(home));
+    home = __builtin_amdgcn_readfirstlane(home) & (kPoolHeads - 1);
+    // One pool ticket from head h (lane 0's vector atomic, device scope): the returned index, or
+    // UINT32_MAX past the head's share.  Its return is waited on where the value is first used.
+    auto pool_fetch = [&](uint32_t h) -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0)
+            v = __hip_atomic_fetch_add(pool + h * kPoolStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v;
+    };
+    auto pool_group = [&](uint32_t h, uint32_t v) -> uint64_t {   // n_groups when head h is exhausted
+        v = __builtin_amdgcn_readfirstlane(v);
+        const uint64_t p = uint64_t(v) * kPoolHeads + h;
+        const uint64_t r = p < pool_n ? own_end + p : n_groups;
+        return (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(r >> 32))))) << 32) |
+               uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(r))));
+    };
+    auto home_open = [&]() {                                   // home head not yet found empty
+        return !(__builtin_amdgcn_readfirstlane(__hip_atomic_load(&pool_empty, __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) & (1u << home));
+    };
+    // The rest of the sweep, synchronous (only once the home head is empty: the end of the launch).
+    auto pool_sweep = [&](uint32_t h0) -> uint64_t {
+        __hip_atomic_fetch_or(&pool_empty, 1u << h0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint64_t gp = n_groups;
+        for (uint32_t i = 1; i < kPoolHeads; i++) {
+            const uint32_t h = (h0 + i) & (kPoolHeads - 1);
+            const uint32_t known = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&pool_empty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (gp < n_groups || (known & (1u << h)))
+                continue;
+            gp = pool_group(h, pool_fetch(h));
+            if (gp >= n_groups)                                // every lane: an idempotent LDS or
+                __hip_atomic_fetch_or(&pool_empty, 1u << h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return gp;
+    };
     auto take = [&]() -> uint64_t {                            // DYN: the next group of this workgroup
         uint32_t tk = 0;
         if (lane == 0)
             tk = __hip_atomic_fetch_add(&next_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         tk = __builtin_amdgcn_readfirstlane(tk);
-        return uint64_t(blockIdx.x) + uint64_t(tk) * gridDim.x;
+        const uint64_t gt = uint64_t(blockIdx.x) + uint64_t(tk) * gridDim.x;
+        return POOL && gt >= own_end ? ~uint64_t(0) : gt;     // POOL: ~0 = "from the pool"
+    };
+    // POOL epilogue: every wave counts itself out; the workgroup's last wave counts the workgroup out
+    // and the launch's last workgroup zeroes the heads and the count for the slot's next launch.
+    auto pool_done = [&]() {
+        if (!POOL)
+            return;
+        uint32_t last = 0;
+        if (lane == 0)
+            last = __hip_atomic_fetch_add(&waves_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == WAVES - 1;
+        if (!__builtin_amdgcn_readfirstlane(last))
+            return;
+        uint32_t wg_last = 0;
+        if (lane == 0)
+            wg_last = __hip_atomic_fetch_add(pool + kPoolHeads * kPoolStride, 1u, __ATOMIC_ACQ_REL,
+                                             __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        if (__builtin_amdgcn_readfirstlane(wg_last) && lane <= kPoolHeads)
+            __hip_atomic_store(pool + lane * kPoolStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     uint64_t g = DYN ? uint64_t(blockIdx.x) + uint64_t(wv) * gridDim.x : wave0;
-    if (g >= n_groups)
+    if (POOL && g >= own_end && g < n_groups) {               // fewer own rounds than waves
+        g = pool_group(home, pool_fetch(home));
+        if (g >= n_groups)
+            g = pool_sweep(home);
+    }
+    if (g >= n_groups) {
+        pool_done();
         return;
+    }
     const uint32_t my_off = wv * 2 * SLOT;                     // slot 0; slot 1 = my_off + SLOT (bit 13 clear)
     const uint32_t lds0 = uint32_t(reinterpret_cast<uintptr_t>(ring)) + my_off;
     const uint32_t nfull = rec_len >> 6, t = rec_len & 63;
@@ -243,6 +340,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // barrier hipcc hoisted the window tables (~300 VALU) above the first DMA.
     __builtin_amdgcn_sched_barrier(0);
     uint64_t gn = DYN ? take() : g + wstride;                  // the group after g
+    // POOL: gn == ~0 -> the head's ticket is requested in iteration 1 (pv) and resolved at the end
+    uint32_t pv = 0;
+    bool pv_pending = false;
     win_setup(g);
     uint32_t tm[16], tp[16];
     tail_masks(t, tm, tp);
@@ -270,6 +370,27 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     for (;;) {
         typename Alg::State st = Alg::iv();
         uint32_t k = 1;
+        if (POOL && gn == ~uint64_t(0) && K >= 2) {
+            // iteration 1 with the pool ticket requested behind its refill: the return is waited on
+            // with iteration 2's line, after blocks 0 and 1 are hashed
+            BRB_LINE_PROBE(1);
+            brb_dma::wait_vmcnt<0>();
+            read_window(ae);
+            BRB_LINE_PROBE(2);
+            issue(vq, rs, so, 0);
+            pv_pending = home_open();
+            if (pv_pending)
+                pv = pool_fetch(home);
+            __builtin_amdgcn_sched_barrier(0);
+            Alg::compress(st, w0);
+            Alg::compress(st, w1);
+            __builtin_amdgcn_sched_barrier(0);
+            k = 2;
+            if (k + 1 <= K - 1) {                              // keep the loop's parity: k odd there
+                full_step(st, ao, 1);
+                k = 3;
+            }
+        }
         for (; k + 2 <= K; k += 2) {
             full_step(st, ae, 0);                              // odd k: line k+1 goes to slot 0
             full_step(st, ao, 1);                              // even k: line k+1 goes to slot 1
@@ -286,6 +407,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             brb_dma::wait_vmcnt<0>();
             read_window(al);
             BRB_LINE_PROBE(2);
+            if (POOL && gn == ~uint64_t(0)) {                  // the pool ticket (K = 1: taken here)
+                gn = pv_pending || home_open() ? pool_group(home, pv_pending ? pv : pool_fetch(home)) : n_groups;
+                pv_pending = false;
+                if (gn >= n_groups)
+                    gn = pool_sweep(home);
+            }
             if (gn < n_groups) {
                 dma_setup(gn, vqn, rsn);
                 son = 0;
@@ -310,6 +437,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         win_setup(g);
     }
     BRB_LINE_PROBE(3);
+    pool_done();
 }
 
 // Line-aligned staging needs 4-byte record bases (the window shift is whole dwords).
@@ -329,11 +457,50 @@ inline unsigned device_cu_count()
     return n;
 }
 
+// POOL: the pool heads of the next pooled launch on the calling thread's device -- slot
+// (launches so far) mod kPoolSlots of a per-device ring, zeroed once at allocation and by every
+// launch's last workgroup after that.  A slot is reused kPoolSlots launches later: launches on one
+// stream run in order, and more than kPoolSlots pooled launches in flight on one device at once
+// (across streams) are not expected.  nullptr if the ring cannot be had (the launch then runs
+// without the pool).
+inline uint32_t *pool_slot(hipStream_t s)
+{
+    constexpr int kMaxDev = 64;
+    static std::mutex mu;
+    static uint32_t *ring[kMaxDev] = {};
+    static std::atomic<uint64_t> next[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev)
+        return nullptr;
+    uint32_t *r = __atomic_load_n(&ring[dev], __ATOMIC_ACQUIRE);
+    if (!r) {
+        std::lock_guard<std::mutex> lk(mu);
+        r = ring[dev];
+        if (!r) {
+            void *p = nullptr;
+            const size_t bytes = size_t(kPoolSlots) * kPoolSlotWords * 4;
+            if (hipMalloc(&p, bytes) != hipSuccess || hipMemsetAsync(p, 0, bytes, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess) {
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            r = static_cast<uint32_t *>(p);
+            __atomic_store_n(&ring[dev], r, __ATOMIC_RELEASE);
+        }
+    }
+    return r + (next[dev].fetch_add(1, std::memory_order_relaxed) % kPoolSlots) * kPoolSlotWords;
+}
+
+// Rounds of groups (one group per workgroup per round) that a launch leaves to the pool: test
+// option line_pool (-1 = this default).
+constexpr int kDefaultPoolRounds = 8;
+
 // One 8-wave workgroup per CU (128 KiB of LDS), persistent, groups handed out by tickets (DYN), DMA
 // with the non-temporal policy (every line is read exactly once).  Measured with
 // tools/mb/md5_ab.hip, MD5, medians of 20-launch bursts:
 //   1 Mi x 1500 B: 316 us static 4-wave workgroups -> 300 us (read floor of the same bytes: 261 us nt)
 //   cfg2 65 536 x 1500 B: 25.3 us (record-relative 128-byte stages) -> 24.9 us
+// Batches of at least 2 x (pooled rounds) rounds balance their tail through the pool (POOL above).
 template <class Alg>
 hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_rec, uint8_t *out, bool out_al,
                              hipStream_t s)
@@ -341,10 +508,20 @@ hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_r
     constexpr int W = 8;
     const uint64_t groups = (n_rec + 63) / 64;
     const unsigned g = unsigned(groups < device_cu_count() ? groups : device_cu_count());
-    if (out_al)
-        digest_line_kernel<Alg, W, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+    const uint64_t rounds = (groups + g - 1) / g;
+    int pr = brb_opt::get(brb_opt::kLinePool);
+    if (pr < 0)
+        pr = kDefaultPoolRounds;
+    uint32_t *slot = pr > 0 && rounds >= 2 * uint64_t(pr) ? pool_slot(s) : nullptr;
+    const uint32_t t_own = slot ? uint32_t(rounds - uint64_t(pr)) : 0u;
+    if (slot && out_al)
+        digest_line_kernel<Alg, W, true, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out, slot, t_own);
+    else if (slot)
+        digest_line_kernel<Alg, W, false, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out, slot, t_own);
+    else if (out_al)
+        digest_line_kernel<Alg, W, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out, nullptr, 0u);
     else
-        digest_line_kernel<Alg, W, false, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out);
+        digest_line_kernel<Alg, W, false, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out, nullptr, 0u);
     return hipGetLastError();
 }
 

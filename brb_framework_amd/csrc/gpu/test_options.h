@@ -25,13 +25,15 @@ enum Opt {
     kLineSlots = 10,    // LDS-DMA ring slots of the line-staged kernels: 2 or 3; 0 = each kernel's default
     kRc4Pair = 11,      // 1: RC4+MD5 frame / open on keystream + partner wave pairs (default); 0: one wave
     kRc4CryptPair = 12, // 1: the RC4 pass on keystream + I/O wave pairs; 0: one wave per stream does both
-    kPairStall = 13,    // 1: inject a protocol fault into the segment-digest, MetaData and RC4-pass wave pairs
+    kPairStall = 13,    // 1: inject a protocol fault into the segment-digest, MetaData, RC4-pass and frame/open wave pairs
                         // (the first workgroup's first pair never hands over its first plan / block), so the
                         // tests see a bounded wait give up and the call report it (pair_fault.h); 0: off
-    kCount = 14
+    kLinePool = 14,     // fixed-stride line digests: rounds of groups left to the chip-wide tail pool
+                        // (digest_line.h POOL); -1 the launcher's default, 0 no pool
+    kCount = 15
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0, -1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -228,6 +228,50 @@ def test_line_kernel_short_groups(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
+@pytest.mark.parametrize("n,rec_len,pool", [
+    (300_001, 1500, 1),      # 4 688 groups over 256 workgroups: 19 rounds, the last one pooled
+    (300_001, 260, 8),       # K = 3, 8 of 19 rounds pooled, a partial last group
+    (70_000, 68, 2),         # K = 1: the pool ticket is taken at the last (only) iteration
+    (70_000, 196, 2),        # K = 2: the ticket requested in iteration 1, iteration 2 the last
+    (1 << 20, 1500, 32),     # the cfg5 shard, half of it pooled
+    (1 << 20, 1500, 0),      # ... and without the pool
+])
+def test_line_pool_tail(brb, orc, torch_dev, n, rec_len, pool):
+    """The line kernel's chip-wide tail pool (digest_line.h POOL, test option line_pool = rounds
+    pooled): every digest against the oracle, three launches back to back (each launch's last
+    workgroup zeroes the heads its slot's next user starts from)."""
+    data = workload.gen_records(0x5EED0015, 0, n, rec_len)
+    d = to_dev(torch_dev, data)
+    want = orc.md5_batch_fixed(data, rec_len, n, threads=16)
+    with brb.TestOption("line_pool", pool):
+        for _ in range(3):
+            assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want)
+        assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),
+                              orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+
+
+def test_line_pool_slot_ring_wraps(brb, orc, torch_dev):
+    """More pooled launches than the ring has slots (kPoolSlots = 512), alternating over two
+    streams: every launch still equals the oracle, so every slot was left zeroed for its next user."""
+    torch = torch_dev
+    n, L = 256 * 64 * 2, 68                      # two rounds of groups: one pooled
+    data = workload.gen_records(0x5EED0016, 0, n, L)
+    d = to_dev(torch, data)
+    want = torch.from_numpy(orc.md5_batch_fixed(data, L, n, threads=16)).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(8)]
+    bad = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in streams]   # one per stream
+    with brb.TestOption("line_pool", 1):
+        for i in range(1100):
+            s = streams[i % 2]
+            with torch.cuda.stream(s):
+                o = outs[i % 8]
+                brb.md5_batch_fixed(d, L, n, out=o, stream=s, async_=True)
+                bad[i % 2] += (o != want).any().to(torch.int64)
+    torch.cuda.synchronize()
+    assert [int(b) for b in bad] == [0, 0]
+
+
 @pytest.mark.parametrize("rec_len", [1500, 1501])
 def test_many_groups_per_wave(brb, orc, torch_dev, rec_len):
     """Batches large enough that every wave takes several 64-record groups from its workgroup's

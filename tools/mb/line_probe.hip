@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 __device__ uint64_t *g_probe;
@@ -65,10 +66,24 @@ struct AlgNull : AlgLit {
 };
 
 using Kern = void (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *);
-// launches a kernel of the four arguments (data, rec_len, n_rec, out)
-static void launch(const void *k, unsigned grid, unsigned bs, const uint8_t *src, uint32_t L, uint64_t n, uint8_t *o)
+using KernL = void (*)(const uint8_t *, uint32_t, uint64_t, uint8_t *, uint32_t *, uint32_t);
+// pool heads for the POOL line kernel: a ring of slots, each zeroed by its launch's last workgroup
+static uint32_t *g_pool_ring;
+static uint64_t g_pool_next;
+// launches a kernel of the four arguments (data, rec_len, n_rec, out), or a line kernel of six
+// (+ pool slot, owned rounds; pool_rounds < 0: a kernel of four arguments)
+static void launch(const void *k, unsigned grid, unsigned bs, const uint8_t *src, uint32_t L, uint64_t n, uint8_t *o,
+                   int pool_rounds = -1)
 {
-    void *args[] = {&src, &L, &n, &o};
+    if (pool_rounds < 0) {
+        void *args[] = {&src, &L, &n, &o};
+        if (hipLaunchKernel(k, dim3(grid), dim3(bs), args, 0, 0) != hipSuccess) { printf("launch failed\n"); exit(1); }
+        return;
+    }
+    const uint64_t groups = (n + 63) / 64, rounds = (groups + grid - 1) / grid;
+    uint32_t *slot = g_pool_ring + (g_pool_next++ % brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords;
+    uint32_t t_own = uint32_t(rounds - uint64_t(pool_rounds));
+    void *args[] = {&src, &L, &n, &o, &slot, &t_own};
     if (hipLaunchKernel(k, dim3(grid), dim3(bs), args, 0, 0) != hipSuccess) { printf("launch failed\n"); exit(1); }
 }
 
@@ -95,29 +110,42 @@ int main(int argc, char **argv)
     CK(hipMalloc(&pr, 4096 * NP * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
     struct V { const char *name; Kern k; };
-    struct VG { const char *name; const void *k; int waves; };
+    struct VG { const char *name; const void *k; int waves; int pool = -1; };
+    CK(hipMalloc(&g_pool_ring, size_t(brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords * 4));
+    CK(hipMemset(g_pool_ring, 0, size_t(brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords * 4));
     VG vs64[] = {{"DMA64 static 4x4", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4},
                  {"DMA64 dyn16", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
                  {"DMA64 dyn8", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
                  {"DMA64 only", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
     // waves = -4: digest_line1_kernel (one group per wave, 4-wave workgroups, grid = groups / 4)
-    VG vs[] = {{"LINE md5 nt dyn8", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+    // argv[3] = "pool": the product line kernel without and with the tail pool (4 / 8 / 16 rounds),
+    // interleaved twice (the workgroup-end spread)
+    VG vp[] = {{"LINE nopool", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE pool8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
+               {"LINE pool4", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
+               {"LINE pool16", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16},
+               {"LINE nopool #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE pool8 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
+               {"LINE pool4 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
+               {"LINE pool16 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16}};
+    VG vs[] = {{"LINE md5 nt dyn8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
               {"LINE1 ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
               {"LINE1 ns2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
               {"LINE1 ns2 u4", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
               {"LINE1 ns3 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3, true>, -4},
               {"LINE1 ns2 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, true>, -4},
-              {"LINE md5 nt dyn8 #2", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8},
+              {"LINE md5 nt dyn8 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
               {"LINE1 ns3 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
               {"LINE1 ns2 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
               {"LINE1 ns2 u4 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
               {"LINE1 dma-only ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
-              {"LINE dma-only nt dyn8", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8}};
+              {"LINE dma-only nt dyn8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8, 0}};
     int it = 0;
     const bool small = L <= 64;
-    const int nv = small ? 4 : int(sizeof(vs) / sizeof(vs[0]));
+    const bool pool = argc > 3 && std::string(argv[3]) == "pool";
+    const int nv = small ? 4 : pool ? int(sizeof(vp) / sizeof(vp[0])) : int(sizeof(vs) / sizeof(vs[0]));
     for (int vi = 0; vi < nv; vi++) {
-        const VG &v = small ? vs64[vi] : vs[vi];
+        const VG &v = small ? vs64[vi] : pool ? vp[vi] : vs[vi];
         // 4-wave workgroups: 2 per CU (4 for <= 64 B records); bigger (dyn): one per CU
         const unsigned grid = v.waves == -4 ? unsigned((groups + 3) / 4)
                               : v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, small ? 1024 : 512))
@@ -131,16 +159,16 @@ int main(int argc, char **argv)
         float tot = 0;
         while (tot < 500.f) {
             hipEventRecord(a);
-            for (int i = 0; i < 50; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
+            for (int i = 0; i < 50; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o, v.pool);
             hipEventRecord(b);
             CK(hipEventSynchronize(b));
             float ms;
             hipEventElapsedTime(&ms, a, b);
             tot += ms;
         }
-        for (int i = 0; i < 9; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
+        for (int i = 0; i < 9; i++) launch(v.k, grid, bs, d[it++ % nrot], L, n, o, v.pool);
         CK(hipMemsetAsync(pr, 0, 4096 * NP * 8));
-        launch(v.k, grid, bs, d[it++ % nrot], L, n, o);
+        launch(v.k, grid, bs, d[it++ % nrot], L, n, o, v.pool);
         CK(hipDeviceSynchronize());
         std::vector<uint64_t> all(4096 * NP), hp;
         CK(hipMemcpy(all.data(), pr, all.size() * 8, hipMemcpyDeviceToHost));
