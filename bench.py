@@ -96,30 +96,62 @@ def relaunch_distributed(args) -> None:
     sys.exit(subprocess.call(cmd))
 
 
+def cgroup_cpu_quota():
+    """The lease's CPU quota from the cgroup (v2 cpu.max "<quota> <period>" or "max <period>"; v1
+    cpu.cfs_quota_us / cpu.cfs_period_us): (cpus or None when unlimited, the raw text)."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            raw = open(path).read().strip()
+        except OSError:
+            continue
+        q, _, per = raw.partition(" ")
+        return (None if q == "max" else float(q) / float(per or 100000)), f"{path}: {raw}"
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q < 0 else q / per), f"cgroup v1 cfs_quota_us {q} cfs_period_us {per}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu quota file"
+
+
 def cpu_threads() -> int:
-    """Threads for the CPU baseline: the lease's CPU share.  On the GPU box the affinity mask shows
-    the whole host (256 CPUs) while one GPU's share is 16 (OMP_NUM_THREADS / MAX_JOBS are set to it
-    and the harness asks for pools of that size); here the container's own CPUs."""
+    """Threads for the CPU baseline: the lease's CPU share.  A finite cgroup quota decides when it
+    has one (floor of quota / period); otherwise the share the harness declares in OMP_NUM_THREADS /
+    MAX_JOBS (16 per GPU on the box, where the affinity mask shows the whole 256-CPU host); otherwise
+    the affinity mask (this container)."""
+    aff = len(os.sched_getaffinity(0))
+    quota, _ = cgroup_cpu_quota()
+    if quota is not None:
+        return max(1, min(aff, int(quota)))
     for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
         if os.environ.get(var, "").isdigit():
-            return max(1, int(os.environ[var]))
-    return max(1, len(os.sched_getaffinity(0)))
+            return max(1, min(aff, int(os.environ[var])))
+    return max(1, aff)
+
+
+NOTES = {}     # attached to the bench line as "notes": context that is not a measurement
 
 
 def core_counts(threads: int, single_core_rate: float) -> dict:
-    """`cores` = threads actually used, beside `nproc` (as printed by the tool) and the affinity
-    mask; the whole-mask figure is a LINEAR EXTRAPOLATION of the measured single-core rate, labelled
-    as such (running 256 threads would exceed the lease's CPU share)."""
+    """`cores` = threads actually used, with the evidence for that number: the cgroup quota, the
+    affinity mask, nproc and the declared share.  The whole-mask linear extrapolation of the
+    single-core rate is NOT part of the baseline: it goes to the line's "notes", labelled."""
     try:
         nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout.strip())
     except (OSError, ValueError, subprocess.SubprocessError):
         nproc = None
     aff = len(os.sched_getaffinity(0))
-    return {"cores": threads, "nproc": nproc, "affinity_cpus": aff,
-            "all_affinity_cpus_extrapolated": round(single_core_rate * aff, 3),
-            "cores_note": f"measured on {threads} threads (the lease's CPU share); nproc={nproc} "
-                          f"(honours OMP_NUM_THREADS); affinity mask {aff} CPUs; "
-                          "all_affinity_cpus_extrapolated = single-core rate x affinity CPUs, not measured"}
+    quota, quota_raw = cgroup_cpu_quota()
+    declared = {v: os.environ[v] for v in ("OMP_NUM_THREADS", "MAX_JOBS") if v in os.environ}
+    NOTES["cpu_all_affinity_cpus_extrapolated_gib_s"] = {
+        "value": round(single_core_rate * aff, 3),
+        "what": f"single-core rate x {aff} affinity CPUs: a linear extrapolation, NOT measured, not the baseline"}
+    why = (f"cgroup quota {quota:g} CPUs" if quota is not None else
+           f"cgroup quota unlimited ({quota_raw}); the lease's declared share {declared}" if declared else
+           f"cgroup quota unlimited ({quota_raw}); the affinity mask")
+    return {"cores": threads, "cores_evidence": {"cgroup_cpu_max": quota_raw, "cgroup_quota_cpus": quota,
+                                                 "affinity_cpus": aff, "nproc": nproc, "declared_share": declared,
+                                                 "threads_used_because": why}}
 
 
 def kernel_id(name: str) -> str:
@@ -362,6 +394,8 @@ def main():
     else:
         result = bench_digest(args, cfg_id, cfg, rank, world, dev, stream, barrier, max_over_ranks, log)
     if rank == 0:
+        if NOTES:
+            result["notes"] = NOTES
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()

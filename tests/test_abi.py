@@ -174,3 +174,33 @@ def test_missing_symbol_raises_by_name(brb, monkeypatch):
     stub = crypto._missing_symbol("BRB_NoSuchCall")
     with pytest.raises(RuntimeError, match="BRB_NoSuchCall"):
         stub(1, 2)
+
+
+def test_batcher_and_runtime_refusals(brb):
+    """The transform batcher's and the runtime's argument / refusal paths, reached without a device
+    (and run under ASan + UBSan by tools/sanitize_check.sh): every call with a
+    NULL batcher or a bad argument returns -1 or NULL with a reason, and a fault check with no async
+    call pending is clean."""
+    L = brb.lib()
+    b = ctypes.create_string_buffer(64)
+    assert L.BRB_TransformBatcherCreate(0, 1 << 20, 1) is None and b"max_conns" in L.BRB_CryptoGPU_LastError()
+    assert L.BRB_TransformBatcherCreate(4, 0, 1) is None
+    assert L.BRB_TransformBatcherCreate(4, 1 << 20, 7) is None and b"algo" in L.BRB_CryptoGPU_LastError()
+    assert L.BRB_TransformBatcherRead(None, 0, b, 8) == -1
+    assert L.BRB_TransformBatcherWrite(None, 0, b, 8, 1) == -1
+    assert L.BRB_TransformBatcherEnable(None, 0, b"k", 1) == -1
+    assert L.BRB_TransformBatcherFlush(None, None, None) == -1
+    assert L.BRB_TransformBatcherFlushAsync(None, None, None) == -1
+    assert L.BRB_TransformBatcherInjectFault(None, 0) == -1
+    st = brb.BRB_RC4_State()
+    assert L.BRB_TransformBatcherGetState(None, 0, 0, ctypes.byref(st)) == -1
+    L.BRB_TransformBatcherDestroy(None)
+    assert L.BRB_CryptoGPU_HostRegister(None, 64) == -1
+    assert L.BRB_CryptoGPU_HostUnregister(b) == -1 and b"not registered" in L.BRB_CryptoGPU_LastError()
+    assert L.BRB_CryptoGPU_AsyncFaultCheck() == 1
+    if not brb.gpu_available():
+        assert L.BRB_TransformBatcherCreate(4, 1 << 20, 1) is None and L.BRB_CryptoGPU_LastError()
+        assert L.BRB_TransformBatcherCreate(4, 1 << 20, 2 | brb.BATCHER_ALL_DEVICES) is None
+        assert L.BRB_MemBufferEncrypt(b, 16, 7, 0, ctypes.byref(ctypes.c_ulong(0)), 0, None) == 0
+        assert L.BRB_MetaDataUnpackBatch(b, b, b, 1, b, 0, None) == 0
+        assert L.BRB_MD5BatchSegments(b, b, b, b, 1, b, 0, None) == 0
