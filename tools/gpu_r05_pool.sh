@@ -18,3 +18,5 @@ for r in 1 2 3; do
 done
 timeout -k 10 200 python3 bench.py --no-cpu-baseline --no-pcie --no-cfg5 > $O/cfg2.json 2> $O/cfg2.err && python3 -c "import json; d=json.load(open('$O/cfg2.json')); r=d['roofline']; print('cfg2', round(r['launch_us_avg'],2), r['frac'])"
 timeout -k 10 300 tools/mb/lprobe5 1048576 1500 pool > $O/lprobe_pool.txt 2>&1; grep -E "^LINE|per-WG" $O/lprobe_pool.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log
