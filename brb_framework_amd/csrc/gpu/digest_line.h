@@ -386,8 +386,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             Alg::compress(st, w1);
             __builtin_amdgcn_sched_barrier(0);
             k = 2;
-            if (k + 1 <= K - 1) {                              // keep the loop's parity: k odd there
-                full_step(st, ao, 1);
+            if (k < K) {                                       // iteration 2 (even) is a full step too:
+                full_step(st, ao, 1);                          // the loop below then starts at odd k
                 k = 3;
             }
         }

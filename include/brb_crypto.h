@@ -414,7 +414,9 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * partner wave pairs / one wave per connection), "rc4_pair" 1/0 (BRB_RC4_CryptBatch likewise; a forced
  * "rc4_sector" value selects the one-wave kernel), "pair_stall" 0/1 (1: the segment, MetaData, RC4
  * pass and RC4+MD5 frame / open wave pairs get a protocol fault injected, so the call returns
- * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped).  Returns 1 and the previous
+ * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped), "line_pool" -1/0/k
+ * (fixed-stride line digests of large batches: the launcher's default number of group rounds left to
+ * the chip-wide tail pool / no pool / k rounds).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

@@ -233,6 +233,8 @@ def test_line_kernel_short_groups(brb, orc, torch_dev, n, rec_len, off):
     (300_001, 260, 8),       # K = 3, 8 of 19 rounds pooled, a partial last group
     (70_000, 68, 2),         # K = 1: the pool ticket is taken at the last (only) iteration
     (70_000, 196, 2),        # K = 2: the ticket requested in iteration 1, iteration 2 the last
+    (300_001, 260, 4),       # K = 3: iterations 1 and 2 full, the loop below starts at k = 3
+    (300_001, 388, 4),       # K = 4
     (1 << 20, 1500, 32),     # the cfg5 shard, half of it pooled
     (1 << 20, 1500, 0),      # ... and without the pool
 ])
