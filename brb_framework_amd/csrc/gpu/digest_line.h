@@ -492,8 +492,13 @@ inline uint32_t *pool_slot(hipStream_t s)
 }
 
 // Rounds of groups (one group per workgroup per round) that a launch leaves to the pool: test
-// option line_pool (-1 = this default).
-constexpr int kDefaultPoolRounds = 8;
+// option line_pool (-1 = this default).  0: measured slower than no pool on the cfg5 shard
+// (interleaved, three rounds, profiles/r05/ab/pool: 286.7 us without, 288.5 / 290.4 / 291.3 us with
+// 4 / 8 / 16 rounds pooled).  The pool evens the workgroups' ends (per-WG end spread p50 30.0 ->
+// 20.8 us with 16 rounds) but not the last one: the launch still ends one group-time (~30 us at two
+// waves per SIMD) after its last group was handed out, and the pool's atomics and its iteration-1
+// step cost more than the earlier workgroups' slack.  Kept as a test option for the A/B.
+constexpr int kDefaultPoolRounds = 0;
 
 // One 8-wave workgroup per CU (128 KiB of LDS), persistent, groups handed out by tickets (DYN), DMA
 // with the non-temporal policy (every line is read exactly once).  Measured with
