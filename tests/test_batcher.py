@@ -322,19 +322,25 @@ def test_states_survive_busy_default_stream(brb, orc, torch_dev):
     b.close()
 
 
+@pytest.mark.parametrize("all_devices", [False, True])
 @pytest.mark.parametrize("pipelined", [False, True])
 @pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("algo", [1, 2])
-def test_pair_fault_round_dropped(brb, orc, torch_dev, algo, zero_copy, pipelined):
+def test_pair_fault_round_dropped(brb, orc, torch_dev, algo, zero_copy, pipelined, all_devices):
     """A wave-pair protocol fault inside a batcher round (test option pair_stall, on the pair kernels
     the rounds run: the RC4 pass, the RC4+MD5 frame and open) drops the round: every buffer comes
     back with valid = BRB_TRANSFORM_DROPPED and no output, Flush returns BRB_BATCH_DROPPED -- no
     plaintext, frame or valid flag computed over wrong bytes is delivered (ev_kq_aio_transform.c:
-    157-184 must never pass over them).  After re-keying (Enable) the next round equals the oracle."""
+    157-184 must never pass over them).  After re-keying (Enable) the next round equals the oracle.
+    all_devices: BRB_BATCHER_ALL_DEVICES forced into two parts (test option "devices"): every part's
+    round is dropped (callbacks come part by part, so results are compared as sets of (conn, op):
+    one buffer per connection and direction here)."""
     rng = np.random.default_rng(100 + algo)
-    C = 96                                        # > 64: the stalled wave's group and ordinary ones
+    C = 192                                       # > 64 per part: the stalled wave's group and ordinary ones
     keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(C)]
-    b = brb.TransformBatcher(C, 4 << 20, algo, zero_copy=zero_copy, pipelined=pipelined)
+    with brb.TestOption("devices", 2 if all_devices else 0):
+        b = brb.TransformBatcher(C, 4 << 20, algo, zero_copy=zero_copy, pipelined=pipelined, all_devices=all_devices)
+    same = (lambda x, y: sorted(x) == sorted(y)) if all_devices else (lambda x, y: x == y)
 
     def rekey():
         for c in range(C):
@@ -375,11 +381,15 @@ def test_pair_fault_round_dropped(brb, orc, torch_dev, algo, zero_copy, pipeline
         with pytest.raises(RuntimeError, match="wave-pair protocol fault.*dropped") as ei:
             b.flush()
     assert ei.value.code == brb.BATCH_DROPPED
-    assert ei.value.results == dropped
+    assert same(ei.value.results, dropped)
     assert b.flush() == []                        # the dropped round is gone, nothing re-runs
     ours_r, ours_w, peer_w = rekey()              # its connections are re-keyed, as after a lost buffer
     expect = submit(1, ours_r, ours_w, peer_w)
-    _check_round(b.flush(), expect, 1)
+    got = b.flush()
+    if all_devices:
+        assert same(got, expect)
+    else:
+        _check_round(got, expect, 1)
     for c in range(0, C, 5):
         assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
     b.close()
