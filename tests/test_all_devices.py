@@ -154,6 +154,19 @@ def test_base64_segments_all_devices(brb, orc, torch_dev, parts):
 
 
 @pytest.mark.gpu
+def test_line_pool_forced_parts(brb, orc, torch_dev):
+    """The line kernel's tail pool (test option line_pool) under the host-mode split: three parts on
+    their worker threads, each launch taking a slot of its device's pool ring concurrently with
+    the others (300 001 records: ~100 000 per part, 7 rounds of groups, the last 2 pooled), twice."""
+    L, n = 1500, 300_001
+    data = workload.gen_records(0x5EED00C4, 0, n, L)
+    want = orc.md5_batch_fixed(data, L, n, threads=8)
+    with brb.TestOption("devices", 3), brb.TestOption("line_pool", 2):
+        for _ in range(2):
+            assert np.array_equal(brb.md5_batch_fixed(data, L, n, all_devices=True), want)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("parts", [3])
 def test_digests_blowfish_forced_parts(brb, orc, torch_dev, parts):
     """The advisor's round-2 item: the concurrent split (worker threads, Pending, per-part results)

@@ -662,3 +662,37 @@ def test_async_pair_fault_check(brb, orc, torch_dev):
     brb.async_fault_check()
     want_st, want = _oracle_crypt(orc, states, data, offs, lens)
     assert np.array_equal(td.cpu().numpy(), want) and np.array_equal(ts.cpu().numpy(), want_st)
+
+
+@pytest.mark.gpu
+def test_async_fault_words_are_per_thread(brb, orc, torch_dev):
+    """The async fault report is the calling thread's: a stalled async call on one thread is seen by
+    that thread's check only; another thread's async calls and checks stay clean."""
+    import threading
+    torch = torch_dev
+    n = 128
+    offs, lens, total = _layout([2048] * n)
+    data = workload.gen_records(SEED + 12, 0, 1, total)
+    states = brb.rc4_states(_keys(n, 44))
+    res = {}
+
+    def clean():
+        ts, td = _to(torch, states), _to(torch, data)
+        for _ in range(3):
+            brb.rc4_crypt_batch(ts, td, _to(torch, offs), _to(torch, lens), async_=True)
+        torch.cuda.synchronize()
+        try:
+            brb.async_fault_check()
+            res["clean"] = "ok"
+        except RuntimeError as e:
+            res["clean"] = str(e)
+
+    with brb.TestOption("rc4_pair", 1), brb.TestOption("pair_stall", 1):
+        brb.rc4_crypt_batch(_to(torch, states), _to(torch, data), _to(torch, offs), _to(torch, lens), async_=True)
+    torch.cuda.synchronize()
+    th = threading.Thread(target=clean)
+    th.start()
+    th.join()
+    assert res["clean"] == "ok"
+    with pytest.raises(RuntimeError, match="returned -4"):
+        brb.async_fault_check()
