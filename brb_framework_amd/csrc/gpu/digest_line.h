@@ -105,7 +105,17 @@ constexpr uint32_t kPoolStride = 64;                           // u32: heads 256
 constexpr uint32_t kPoolSlotWords = (kPoolHeads + 1) * kPoolStride;   // the heads, then the done count
 constexpr uint32_t kPoolSlots = 512;
 
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool NT = false, bool DYN = false, bool POOL = false>
+// LOCK (with a static split, DYN = false; round 5): the two waves that share a SIMD progress in
+// lockstep.  Each wave publishes its iteration count in LDS and reads its SIMD partner's (the other
+// wave of the workgroup with the same HW_REG_HW_ID SIMD id) once per iteration; the wave that is
+// ahead by more than one iteration drops to issue priority 0, the one behind rises to 2.  Why: at
+// two waves per SIMD the older wave wins the issue arbitration, and a static split then ends with
+// one wave of every SIMD running alone; with tickets (DYN) the last groups are handed out a group
+// early and the workgroup's waves end one group-time apart (profiles/r05/ab/pool/lprobe_pool.txt:
+// per-WG end spread p50 30 us).  With equal shares (groups a multiple of the grid's waves) and
+// equal progress every wave of a CU ends at about the same time.
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool NT = false, bool DYN = false, bool POOL = false,
+          bool LOCK = false>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data,
                                                                              uint32_t rec_len, uint64_t n_rec,
                                                                              uint8_t *__restrict__ out,
@@ -116,8 +126,45 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     __shared__ __attribute__((aligned(16))) uint8_t ring[WAVES * 2 * SLOT];
     __shared__ uint32_t next_ticket;
     __shared__ uint32_t pool_empty, waves_done;                // POOL: heads found empty; waves finished
+    __shared__ uint32_t lock_simd[WAVES], lock_prog[WAVES];    // LOCK: each wave's SIMD and iterations
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t partner = WAVES;                                  // LOCK: the wave sharing this SIMD (WAVES: none)
+    uint32_t prog = 0;
+    if (LOCK) {
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        if (lane == 0) {
+            lock_simd[wv] = (__builtin_amdgcn_readfirstlane(hw) >> 4) & 3u;
+            lock_prog[wv] = 0;
+        }
+        __syncthreads();
+        const uint32_t me = lock_simd[wv];
+        for (uint32_t w = 0; w < uint32_t(WAVES); w++)
+            if (w != wv && lock_simd[w] == me && partner == uint32_t(WAVES))
+                partner = w;
+        partner = __builtin_amdgcn_readfirstlane(partner);
+    }
+    // LOCK: publish this wave's progress and read the partner's (issued before the iteration's waits,
+    // used after its window read); then set the issue priority from the difference
+    auto lock_pub = [&]() -> uint32_t {
+        if (!LOCK || partner >= uint32_t(WAVES))
+            return 0;
+        ++prog;
+        __hip_atomic_store(&lock_prog[wv], prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __hip_atomic_load(&lock_prog[partner], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto lock_prio = [&](uint32_t other) {
+        if (!LOCK || partner >= uint32_t(WAVES))
+            return;
+        const int d = int(prog - __builtin_amdgcn_readfirstlane(other));
+        if (d > 1)
+            __builtin_amdgcn_s_setprio(0);
+        else if (d < -1)
+            __builtin_amdgcn_s_setprio(2);
+        else
+            __builtin_amdgcn_s_setprio(1);
+    };
     const uint64_t n_groups = (n_rec + 63) / 64;
     const uint64_t wave0 = uint64_t(blockIdx.x) * WAVES + wv;
     const uint64_t wstride = uint64_t(gridDim.x) * WAVES;
@@ -356,8 +403,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // issues ~18 fewer scalar/branch instructions per iteration than one loop with the checks.
     auto full_step = [&](typename Alg::State &st, const uint32_t (&ad)[32], uint32_t refill_slot) {
         BRB_LINE_PROBE(1);
+        const uint32_t other = lock_pub();
         brb_dma::wait_vmcnt<0>();
         read_window(ad);
+        lock_prio(other);
         BRB_LINE_PROBE(2);
         issue(vq, rs, so, refill_slot);
         // Without branches between the steps hipcc interleaved the compressions with the window
@@ -404,8 +453,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
             for (int i = 0; i < 32; i++)
                 al[i] = (K & 1) ? ae[i] : ao[i];
             BRB_LINE_PROBE(1);
+            const uint32_t other = lock_pub();
             brb_dma::wait_vmcnt<0>();
             read_window(al);
+            lock_prio(other);
             BRB_LINE_PROBE(2);
             if (POOL && gn == ~uint64_t(0)) {                  // the pool ticket (K = 1: taken here)
                 gn = pv_pending || home_open() ? pool_group(home, pv_pending ? pv : pool_fetch(home)) : n_groups;
@@ -499,6 +550,7 @@ inline uint32_t *pool_slot(hipStream_t s)
 // waves per SIMD) after its last group was handed out, and the pool's atomics and its iteration-1
 // step cost more than the earlier workgroups' slack.  Kept as a test option for the A/B.
 constexpr int kDefaultPoolRounds = 0;
+constexpr int kDefaultLock = 0;
 
 // One 8-wave workgroup per CU (128 KiB of LDS), persistent, groups handed out by tickets (DYN), DMA
 // with the non-temporal policy (every line is read exactly once).  Measured with
@@ -519,6 +571,20 @@ hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_r
         pr = kDefaultPoolRounds;
     uint32_t *slot = pr > 0 && rounds >= 2 * uint64_t(pr) ? pool_slot(s) : nullptr;
     const uint32_t t_own = slot ? uint32_t(rounds - uint64_t(pr)) : 0u;
+    // LOCK: a static split, every wave of the grid taking every (grid * W)-th group, SIMD partners in
+    // lockstep; for batches of at least two groups per wave (test option line_lock; default kDefaultLock)
+    int lk = brb_opt::get(brb_opt::kLineLock);
+    if (lk < 0)
+        lk = kDefaultLock;
+    if (!slot && lk == 1 && groups >= 2 * uint64_t(g) * W) {
+        if (out_al)
+            digest_line_kernel<Alg, W, true, true, false, false, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out,
+                                                                                        nullptr, 0u);
+        else
+            digest_line_kernel<Alg, W, false, true, false, false, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out,
+                                                                                         nullptr, 0u);
+        return hipGetLastError();
+    }
     if (slot && out_al)
         digest_line_kernel<Alg, W, true, true, true, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out, slot, t_own);
     else if (slot)

@@ -30,10 +30,12 @@ enum Opt {
                         // tests see a bounded wait give up and the call report it (pair_fault.h); 0: off
     kLinePool = 14,     // fixed-stride line digests: rounds of groups left to the chip-wide tail pool
                         // (digest_line.h POOL); -1 the launcher's default, 0 no pool
-    kCount = 15
+    kLineLock = 15,     // fixed-stride line digests of large batches: 1 a static split whose SIMD partners
+                        // progress in lockstep (digest_line.h LOCK), 0 tickets (DYN); -1 the launcher's default
+    kCount = 16
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0, -1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0, -1, -1};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

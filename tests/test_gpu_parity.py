@@ -252,6 +252,25 @@ def test_line_pool_tail(brb, orc, torch_dev, n, rec_len, pool):
                               orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
+@pytest.mark.parametrize("n,rec_len", [
+    (1 << 20, 1500),         # the cfg5 shard: 8 groups per wave exactly
+    (300_001, 260),          # K = 3, 4 688 groups over 2 048 waves (2 or 3 each), a partial last group
+    (1 << 20, 68),           # K = 1
+    (300_001, 196),          # K = 2
+])
+def test_line_lock(brb, orc, torch_dev, n, rec_len):
+    """The static split with SIMD partners in lockstep (digest_line.h LOCK, test option line_lock):
+    every digest against the oracle, MD5 and SHA-1, two launches back to back."""
+    data = workload.gen_records(0x5EED0017, 0, n, rec_len)
+    d = to_dev(torch_dev, data)
+    want = orc.md5_batch_fixed(data, rec_len, n, threads=16)
+    with brb.TestOption("line_lock", 1):
+        for _ in range(2):
+            assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want)
+        assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),
+                              orc.sha1_batch_fixed(data, rec_len, n, threads=16))
+
+
 def test_line_pool_slot_ring_wraps(brb, orc, torch_dev):
     """More pooled launches than the ring has slots (kPoolSlots = 512), alternating over two
     streams: every launch still equals the oracle, so every slot was left zeroed for its next user."""

@@ -119,12 +119,16 @@ int main(int argc, char **argv)
                  {"DMA64 only", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgNull, 4, 2, 1, true>, 4}};
     // waves = -4: digest_line1_kernel (one group per wave, 4-wave workgroups, grid = groups / 4)
     // argv[3] = "pool": the product line kernel without and with the tail pool (4 / 8 / 16 rounds),
-    // interleaved twice (the workgroup-end spread)
+    // the static split with SIMD partners in lockstep (LOCK) and without, interleaved twice (VERDICT
+    // r04 item 2: the workgroup-end spread)
     VG vp[] = {{"LINE nopool", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE lock", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
+               {"LINE static", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false>, 8, 0},
                {"LINE pool8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
                {"LINE pool4", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
                {"LINE pool16", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16},
                {"LINE nopool #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE lock #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
                {"LINE pool8 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
                {"LINE pool4 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
                {"LINE pool16 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16}};
