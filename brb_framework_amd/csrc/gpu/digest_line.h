@@ -154,13 +154,17 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
         __hip_atomic_store(&lock_prog[wv], prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return __hip_atomic_load(&lock_prog[partner], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
+    // The lower-numbered wave of a pair is held `t_own` iterations ahead of its partner, not level
+    // with it: level partners wait for their lines at the same moments, apart each one's wait falls
+    // in the other's compression (cfg5: level 289.9 -> 290.1 us, one iteration 285.5 -> 283.5 us).
+    const int lock_target = wv < partner ? int(t_own) : -int(t_own);   // LOCK: t_own = the lead (iterations)
     auto lock_prio = [&](uint32_t other) {
         if (!LOCK || partner >= uint32_t(WAVES))
             return;
-        const int d = int(prog - __builtin_amdgcn_readfirstlane(other));
-        if (d > 1)
+        const int d = int(prog - __builtin_amdgcn_readfirstlane(other)) - lock_target;
+        if (d > 0)
             __builtin_amdgcn_s_setprio(0);
-        else if (d < -1)
+        else if (d < 0)
             __builtin_amdgcn_s_setprio(2);
         else
             __builtin_amdgcn_s_setprio(1);
@@ -576,13 +580,14 @@ hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_r
     int lk = brb_opt::get(brb_opt::kLineLock);
     if (lk < 0)
         lk = kDefaultLock;
-    if (!slot && lk == 1 && groups >= 2 * uint64_t(g) * W) {
+    if (!slot && lk >= 1 && groups >= 2 * uint64_t(g) * W) {
+        const uint32_t lead = uint32_t(lk);                    // iterations the pair's first wave leads by
         if (out_al)
             digest_line_kernel<Alg, W, true, true, false, false, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out,
-                                                                                        nullptr, 0u);
+                                                                                        nullptr, lead);
         else
             digest_line_kernel<Alg, W, false, true, false, false, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out,
-                                                                                         nullptr, 0u);
+                                                                                         nullptr, lead);
         return hipGetLastError();
     }
     if (slot && out_al)

@@ -30,8 +30,9 @@ enum Opt {
                         // tests see a bounded wait give up and the call report it (pair_fault.h); 0: off
     kLinePool = 14,     // fixed-stride line digests: rounds of groups left to the chip-wide tail pool
                         // (digest_line.h POOL); -1 the launcher's default, 0 no pool
-    kLineLock = 15,     // fixed-stride line digests of large batches: 1 a static split whose SIMD partners
-                        // progress in lockstep (digest_line.h LOCK), 0 tickets (DYN); -1 the launcher's default
+    kLineLock = 15,     // fixed-stride line digests of large batches: k >= 1 a static split whose SIMD partners
+                        // progress in lockstep, the first k iterations ahead (digest_line.h LOCK), 0 tickets
+                        // (DYN); -1 the launcher's default
     kCount = 16
 };
 

@@ -258,13 +258,15 @@ def test_line_pool_tail(brb, orc, torch_dev, n, rec_len, pool):
     (1 << 20, 68),           # K = 1
     (300_001, 196),          # K = 2
 ])
-def test_line_lock(brb, orc, torch_dev, n, rec_len):
-    """The static split with SIMD partners in lockstep (digest_line.h LOCK, test option line_lock):
-    every digest against the oracle, MD5 and SHA-1, two launches back to back."""
+@pytest.mark.parametrize("lead", [1, 4])
+def test_line_lock(brb, orc, torch_dev, n, rec_len, lead):
+    """The static split with SIMD partners in lockstep, the first `lead` iterations ahead
+    (digest_line.h LOCK, test option line_lock = lead): every digest against the oracle, MD5 and
+    SHA-1, two launches back to back."""
     data = workload.gen_records(0x5EED0017, 0, n, rec_len)
     d = to_dev(torch_dev, data)
     want = orc.md5_batch_fixed(data, rec_len, n, threads=16)
-    with brb.TestOption("line_lock", 1):
+    with brb.TestOption("line_lock", lead):
         for _ in range(2):
             assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want)
         assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),

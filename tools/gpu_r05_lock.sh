@@ -10,10 +10,11 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
     -k "line_lock or cfg5_full" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for r in 1 2 3; do
-  for x in 0 1; do
+  for x in ${LOCKS:-0 1 2 4}; do
     timeout -k 10 200 python3 bench.py --records-per-gpu 1048576 --test-option line_lock=$x --no-cpu-baseline --no-pcie --no-cfg5 \
         > $O/cfg5-$x-$r.json 2> $O/cfg5-$x-$r.err || { tail -3 $O/cfg5-$x-$r.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/cfg5-$x-$r.json')); r=d['roofline']; print('cfg5 line_lock=$x', $r, round(r['launch_us_avg'],2), r['frac'])"
   done
 done
-timeout -k 10 300 tools/mb/lprobe5 1048576 1500 pool > $O/lprobe.txt 2>&1; grep -E "^LINE|per-WG" $O/lprobe.txt
+[ -n "$PROBE" ] && { timeout -k 10 300 tools/mb/lprobe5 1048576 1500 pool > $O/lprobe.txt 2>&1; grep -E "^LINE|per-WG" $O/lprobe.txt; }
+true
