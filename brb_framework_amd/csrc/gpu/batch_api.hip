@@ -1109,7 +1109,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1},
                  {"pair_stall", brb_opt::kPairStall, 0, 1},
                  {"line_pool", brb_opt::kLinePool, -1, 64},
-                 {"line_lock", brb_opt::kLineLock, -1, 12}};
+                 {"line_lock", brb_opt::kLineLock, -1, 255}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -157,14 +157,16 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
     // The lower-numbered wave of a pair is held `t_own` iterations ahead of its partner, not level
     // with it: level partners wait for their lines at the same moments, apart each one's wait falls
     // in the other's compression (cfg5: level 289.9 -> 290.1 us, one iteration 285.5 -> 283.5 us).
-    const int lock_target = wv < partner ? int(t_own) : -int(t_own);   // LOCK: t_own = the lead (iterations)
+    // LOCK: t_own = lead (iterations, bits 0-7) | slack << 8 (the drift left to the arbitration)
+    const int lock_target = wv < partner ? int(t_own & 255u) : -int(t_own & 255u);
+    const int lock_slack = int(t_own >> 8);
     auto lock_prio = [&](uint32_t other) {
         if (!LOCK || partner >= uint32_t(WAVES))
             return;
         const int d = int(prog - __builtin_amdgcn_readfirstlane(other)) - lock_target;
-        if (d > 0)
+        if (d > lock_slack)
             __builtin_amdgcn_s_setprio(0);
-        else if (d < 0)
+        else if (d < -lock_slack)
             __builtin_amdgcn_s_setprio(2);
         else
             __builtin_amdgcn_s_setprio(1);
@@ -581,7 +583,7 @@ hipError_t launch_fixed_line(const uint8_t *data, uint32_t rec_len, uint64_t n_r
     if (lk < 0)
         lk = kDefaultLock;
     if (!slot && lk >= 1 && groups >= 2 * uint64_t(g) * W) {
-        const uint32_t lead = uint32_t(lk);                    // iterations the pair's first wave leads by
+        const uint32_t lead = uint32_t(lk & 15) | (uint32_t(lk >> 4) << 8);   // lead | slack << 8
         if (out_al)
             digest_line_kernel<Alg, W, true, true, false, false, true><<<g, 64 * W, 0, s>>>(data, rec_len, n_rec, out,
                                                                                         nullptr, lead);

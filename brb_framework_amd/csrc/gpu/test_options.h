@@ -31,8 +31,8 @@ enum Opt {
     kLinePool = 14,     // fixed-stride line digests: rounds of groups left to the chip-wide tail pool
                         // (digest_line.h POOL); -1 the launcher's default, 0 no pool
     kLineLock = 15,     // fixed-stride line digests of large batches: k >= 1 a static split whose SIMD partners
-                        // progress in lockstep, the first k iterations ahead (digest_line.h LOCK), 0 tickets
-                        // (DYN); -1 the launcher's default
+                        // progress in lockstep, the first (k & 15) iterations ahead, priorities set only past
+                        // a drift of k >> 4 iterations (digest_line.h LOCK); 0 tickets (DYN); -1 the default
     kCount = 16
 };
 
