@@ -93,6 +93,10 @@ struct RowsV {
     uint32_t v[8];
 };
 
+// A row's offset is a multiple of 128 (a line) or kOOB, and its granule's byte offset is below 128,
+// so the voffset is one add of a per-(q mod 4) lane constant; a kOOB row stays >= 2^31, past every
+// descriptor's range (num_records <= 2^31 - 1), so its DMA still returns zeros -- no compare and
+// select per DMA (round 5: 4 VALU -> 1 per DMA, 24 per line).
 BRB_DEV RowsV prep_rows(uint32_t rel, uint32_t lane)
 {
     const uint32_t l3 = lane >> 3;
@@ -101,7 +105,7 @@ BRB_DEV RowsV prep_rows(uint32_t rel, uint32_t lane)
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         const uint32_t rr = uint32_t(__builtin_amdgcn_ds_bpermute(int(8 * q + l3) * 4, int(rel)));
-        r.v[q] = rr >= kOOB ? kOOB : (rr | (q & 1 ? g0 ^ 64u : g0)) + (4096u - 1024u * (q & 3));
+        r.v[q] = rr + ((q & 1 ? g0 ^ 64u : g0) + (4096u - 1024u * (q & 3)));
     }
     return r;
 }
