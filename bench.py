@@ -22,6 +22,7 @@ BASELINE cfg5, 8 388 608 records, at --gpus 8).  Run `python bench.py --help`.
 from __future__ import annotations
 
 import argparse
+import gc
 import hashlib
 import json
 import math
@@ -396,6 +397,8 @@ def main():
     if rank == 0:
         if NOTES:
             result["notes"] = NOTES
+        if SETTLE and "settle" not in result:
+            result["settle"] = SETTLE
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -408,9 +411,27 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
     and ramps over hundreds of ms (cfg2 MD5: 30.4 us per launch after 20 warm-up steps, 25.4 us at
     steady state), and K fills >= timed_s of GPU time.  Step k goes to streams[k % len(streams)].
     Returns (W, K); K is the same on every rank (max over ranks)."""
+    global SETTLE
     n = 0
     step_s = None
     if args.warmup is not None:
+        # settle: the same launches for >= warm_s before the W steps, so a short W (the driver passes
+        # --warmup 5, 0.1 ms of GPU work) does not leave the timed region at a clock still moving:
+        # after the cfg5 leg or on a fresh box the first K = 20 launches ran 22.1 us against 20.5 us
+        # settled (tools/gpu_short_bench.sh, profiles/r05/short/).  Untimed, like the W steps; the
+        # timed region is still exactly K steps.  Recorded on the line as "settle".
+        t0, chunk, m = time.perf_counter(), 4, 0
+        while time.perf_counter() - t0 < warm_s:
+            tc = time.perf_counter()
+            for _ in range(chunk):
+                launch(m, streams[m % len(streams)], m % len(streams))
+                m += 1
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - tc) / chunk
+            chunk = min(chunk * 2, max(4, int(0.1 / max(dt, 1e-7))))
+        SETTLE = {"launches": m, "seconds": round(time.perf_counter() - t0, 3),
+                  "why": "untimed launches of the same step before the W warm-up steps, so the timed region "
+                         "starts at the clock the chip holds under this load (a short W does not reach it)"}
         for k in range(args.warmup):
             launch(k, streams[k % len(streams)], k % len(streams))
         torch.cuda.synchronize()
@@ -441,6 +462,7 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
     return n, int(max_over_ranks(float(k)))
 
 
+SETTLE = None    # warm_up(): the untimed settle before an explicit W (attached to the line)
 MARK = False     # --mark-timed-region
 LAST_ALL_K_S = None   # per-launch seconds of the last timed region over ALL K launches (events)
 
@@ -469,6 +491,8 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
     steady = len(streams) == 1 and n_steps >= 3
+    gc_was = gc.isenabled()
+    gc.disable()         # no collector pause inside a region of a few hundred microseconds
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -484,6 +508,8 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
     e1.record(streams[0])
     torch.cuda.synchronize()
     barrier()
+    if gc_was:
+        gc.enable()
     if MARK:             # sentinel after the region, enqueued after the timing ended
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
