@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-inclusive (PCIe) measurement")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 (1 Mi records per GPU) sub-measurement")
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="with an explicit --warmup: seconds of untimed launches before the W steps (0: none; "
+                         "the PMC passes use 0 so their traces hold only the W + K dispatches)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall-clock budget of the CPU baseline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON with per-launch HBM bytes measured by rocprofv3 --pmc (optional)")
@@ -421,7 +424,8 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
         # settled (tools/gpu_short_bench.sh, profiles/r05/short/).  Untimed, like the W steps; the
         # timed region is still exactly K steps.  Recorded on the line as "settle".
         t0, chunk, m = time.perf_counter(), 4, 0
-        while time.perf_counter() - t0 < warm_s:
+        settle_s = getattr(args, "settle_s", warm_s)
+        while time.perf_counter() - t0 < settle_s:
             tc = time.perf_counter()
             for _ in range(chunk):
                 launch(m, streams[m % len(streams)], m % len(streams))
@@ -429,7 +433,7 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
             torch.cuda.synchronize()
             dt = (time.perf_counter() - tc) / chunk
             chunk = min(chunk * 2, max(4, int(0.1 / max(dt, 1e-7))))
-        SETTLE = {"launches": m, "seconds": round(time.perf_counter() - t0, 3),
+        SETTLE = None if m == 0 else {"launches": m, "seconds": round(time.perf_counter() - t0, 3),
                   "why": "untimed launches of the same step before the W warm-up steps, so the timed region "
                          "starts at the clock the chip holds under this load (a short W does not reach it)"}
         for k in range(args.warmup):
