@@ -495,6 +495,8 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
     steady = len(streams) == 1 and n_steps >= 3
+    for e in (ea, e0, e1):   # torch creates a HIP event at its first record: not inside the region
+        e.record(streams[0])
     gc_was = gc.isenabled()
     gc.disable()         # no collector pause inside a region of a few hundred microseconds
     barrier()
