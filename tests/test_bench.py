@@ -46,14 +46,16 @@ def _fake_torch(clock, kernel_ms):
         def elapsed_time(self, other):
             return other.at - self.at
 
-    cuda = types.SimpleNamespace(Event=Event, synchronize=lambda: None)
+    cuda = types.SimpleNamespace(Event=Event, synchronize=lambda: clock.log.append("sync"))
     return types.SimpleNamespace(cuda=cuda)
 
 
 def test_timed_steps_covers_launches_3_to_k():
     """One stream: e0 is recorded right after launch 2 (it fires when launch 2 ends), e1 after
     launch K, so the per-launch time is (launches 3..K) / (K - 2); the first launches' extra time
-    (modelled as 50 ms and 20 ms stalls) stays out of it."""
+    (modelled as 50 ms and 20 ms stalls) stays out of it.  Every event is recorded once before the
+    synchronize that opens the region (torch creates the HIP event at its first record), so nothing
+    but the launches and their event records sits between the two synchronizes."""
     clock = _Clock()
     torch = _fake_torch(clock, 2.0)
 
@@ -63,7 +65,8 @@ def test_timed_steps_covers_launches_3_to_k():
 
     bench.MARK = False
     wall, per = bench.timed_steps(launch, 5, ["s0"], lambda: None, lambda x: x, torch)
-    assert clock.log == ["event", "launch0", "launch1", "event", "launch2", "launch3", "launch4", "event"]
+    assert clock.log == ["event"] * 3 + ["sync", "event", "launch0", "launch1", "event", "launch2", "launch3",
+                                         "launch4", "event", "sync"]
     assert abs(per - 2.0e-3) < 1e-12          # seconds per launch
     assert abs(bench.LAST_ALL_K_S - (5 * 2.0 + 70.0) / 5 / 1e3) < 1e-12   # all K, the stalls included
     assert wall >= 0
@@ -80,11 +83,12 @@ def test_timed_steps_multi_stream_brackets_all():
 
     bench.MARK = False
     _, per = bench.timed_steps(launch, 4, ["s0", "s1"], lambda: None, lambda x: x, torch)
-    assert clock.log[0] == "event" and clock.log[-1] == "event"
+    region = clock.log[clock.log.index("sync") + 1:-1]
+    assert region[0] == "event" and region[-1] == "event" and region.count("event") == 2
     assert abs(per - 2.0e-3) < 1e-12
     clock.log.clear()
     _, per1 = bench.timed_steps(launch, 1, ["s0"], lambda: None, lambda x: x, torch)
-    assert clock.log == ["event", "launch0", "event"] and abs(per1 - 2.0e-3) < 1e-12
+    assert clock.log == ["event"] * 3 + ["sync", "event", "launch0", "event", "sync"] and abs(per1 - 2.0e-3) < 1e-12
 
 
 # ---- roofline.traffic / roofline.compute come only from a PMC pass of the timed kernels ------------
@@ -174,3 +178,21 @@ def test_committed_evidence_compute_matches_timed_kernels():
     if dirs and checked == 0:
         import pytest
         pytest.skip("no committed evidence with kernel identities yet")
+
+
+def test_warm_up_settles_before_an_explicit_w():
+    """An explicit --warmup W runs after an untimed settle of the same launches (>= settle_s; reported
+    as bench.SETTLE), and --settle-s 0 leaves exactly W launches (the PMC passes)."""
+    import argparse
+    n = [0]
+    log = []
+
+    def launch(k, s, j):
+        n[0] += 1
+    torch = types.SimpleNamespace(cuda=types.SimpleNamespace(synchronize=lambda: log.append(n[0])))
+    w, k = bench.warm_up(argparse.Namespace(warmup=5, steps=20, settle_s=0.05), launch, ["s0"], torch, lambda x: x)
+    assert (w, k) == (5, 20)
+    assert bench.SETTLE and bench.SETTLE["launches"] == n[0] - 5 and bench.SETTLE["seconds"] >= 0.05
+    n[0] = 0
+    w, k = bench.warm_up(argparse.Namespace(warmup=5, steps=20, settle_s=0.0), launch, ["s0"], torch, lambda x: x)
+    assert (w, k) == (5, 20) and n[0] == 5 and bench.SETTLE is None
