@@ -11,6 +11,9 @@ Honesty rules applied here:
     >= 640 MB > the 256 MiB Infinity Cache), so the kernel streams from HBM, not from L3;
   * the timed region is K back-to-back steps, each one C-ABI call (ctypes, arguments resolved
     beforehand), between barrier + synchronize on both sides; value is the whole-job rate (all ranks' bytes / max over ranks of the wall time);
+  * untimed before it: W warm-up steps, after (with an explicit --warmup) a settle of the same
+    launches for >= --settle-s seconds so a short W starts the region at the loaded clock; the
+    line reports the settle ("settle") and W ("warmup") as run;
   * roofline.achieved = bytes per launch / (HIP-event time of the timed region on the launch
     stream / K); digests of the last step are spot-checked against hashlib.
 
