@@ -237,3 +237,38 @@ def test_fuzz_rc4md5_frame_open(brb, orc, torch_dev, seed):
         if i not in bad:
             assert oh[a + H:b].tobytes() == payload[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
     assert np.array_equal(drst.cpu().numpy(), rst)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_host_mode(brb, orc, torch_dev, seed):
+    """The same shapes through host mode (numpy in and out: the library stages the records, runs the
+    kernels and copies the results back): fixed and variable-length digests, segments, RC4."""
+    rng = np.random.default_rng(0xF8C5 + seed)
+    n = int(rng.integers(1, 2000))
+    lens = _lengths(rng, n)
+    offs, size = _layout(rng, lens, overlap=bool(seed & 1))
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    assert np.array_equal(brb.md5_batch(data, offs, lens), orc.md5_batch(data, offs, lens, threads=8))
+    assert np.array_equal(brb.sha1_batch(data, offs, lens), orc.sha1_batch(data, offs, lens, threads=8))
+    rec_len = int(rng.integers(1, 3000))
+    m = size // rec_len
+    if m:
+        fixed = np.ascontiguousarray(data[:rec_len * m])
+        assert np.array_equal(brb.md5_batch_fixed(fixed, rec_len, m), orc.md5_batch_fixed(fixed, rec_len, m, threads=8))
+    k = rng.integers(1, 5, n)
+    first = np.concatenate([[0], np.cumsum(k)]).astype(np.uint64)
+    slens = _lengths(rng, int(first[-1]), hi=900)
+    soffs = (rng.random(len(slens)) * (size - np.minimum(slens, size) + 1)).astype(np.uint64)
+    slens = np.minimum(slens, (size - soffs).astype(np.uint32))
+    got = brb.md5_batch_segments(data, soffs, slens, first)
+    for r in range(0, n, max(1, n // 200)):
+        h = hashlib.md5()
+        for s in range(int(first[r]), int(first[r + 1])):
+            h.update(data[int(soffs[s]):int(soffs[s]) + int(slens[s])].tobytes())
+        assert got[r].tobytes() == h.digest(), (seed, r)
+    if not seed & 1:                              # RC4 in place needs streams that do not overlap
+        st = brb.rc4_states([bytes([i & 255, (i >> 8) & 255, seed]) for i in range(n)])
+        want_d, want_st = data.copy(), st.copy()
+        brb.rc4_crypt_batch(st, data, offs, lens)
+        orc.rc4_crypt_batch(want_st, want_d, offs, lens, threads=8)
+        assert np.array_equal(data, want_d) and np.array_equal(st, want_st)
