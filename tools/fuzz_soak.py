@@ -1,0 +1,38 @@
+"""Soak run of tests/test_gpu_fuzz.py: every fuzz test over fresh seeds until a time budget runs out,
+printing a progress line per round.  Stops at the first mismatch (the seed is in the message).
+    python tools/fuzz_soak.py [seconds] [first_seed]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402
+
+import brb_framework_amd as brb  # noqa: E402
+import oracle  # noqa: E402
+import test_gpu_fuzz as F  # noqa: E402
+
+budget = float(sys.argv[1]) if len(sys.argv) > 1 else 240.0
+seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+brb.lib()
+oracle.lib()
+assert torch.cuda.is_available() and brb.gpu_available()
+t0 = time.time()
+cases = 0
+while time.time() - t0 < budget:
+    F.test_fuzz_fixed_stride(brb, oracle, torch, seed)
+    F.test_fuzz_variable_length(brb, oracle, torch, seed)
+    for sl in (0, 1, 2):
+        F.test_fuzz_segments(brb, torch, seed, sl)
+    F.test_fuzz_rc4(brb, oracle, torch, seed)
+    F.test_fuzz_rc4md5_frame_open(brb, oracle, torch, seed)
+    F.test_fuzz_base64(brb, oracle, torch, seed)
+    F.test_fuzz_blowfish(brb, oracle, torch, seed)
+    F.test_fuzz_host_mode(brb, oracle, torch, seed)
+    cases += 10
+    print(f"seed {seed} ok  ({cases} cases, {time.time() - t0:.0f} s)", flush=True)
+    seed += 1
+print(f"soak: {cases} cases over seeds up to {seed - 1}, no mismatch", flush=True)
