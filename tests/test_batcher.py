@@ -63,8 +63,8 @@ def test_event_loop_after_rc4_and_base64(brb, orc, torch_dev):
     torch.cuda.synchronize()
 
 
-def _event_loop(brb, orc, algo, zero_copy, pipelined):
-    rng = np.random.default_rng(algo)
+def _event_loop(brb, orc, algo, zero_copy, pipelined, seed=None, rounds=6):
+    rng = np.random.default_rng(algo if seed is None else seed)
     C = 300
     keys = [rng.integers(0, 256, int(rng.integers(4, 32)), dtype=np.uint8).tobytes() for _ in range(C)]
     b = brb.TransformBatcher(C, 8 << 20, algo, zero_copy=zero_copy, pipelined=pipelined)
@@ -75,7 +75,7 @@ def _event_loop(brb, orc, algo, zero_copy, pipelined):
     peer_r = [orc.rc4_init(k) for k in keys]      # the peer's read side (consumes what we write)
     for c in range(C):
         b.enable(c, keys[c])
-    for rnd in range(6):
+    for rnd in range(rounds):
         expect = []
         for c in rng.permutation(C)[: int(rng.integers(C // 3, C))]:
             c = int(c)
@@ -121,7 +121,7 @@ def _event_loop(brb, orc, algo, zero_copy, pipelined):
         for c in range(0, C, 7):     # GetState waits for the stream: the running round is included
             assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
     if pipelined:
-        _check_round(b.flush(), pending, 5)
+        _check_round(b.flush(), pending, rounds - 1)
         assert b.flush() == [] and b.flush_async() == []
     b.close()
 

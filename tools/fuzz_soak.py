@@ -1,6 +1,6 @@
 """Soak run of tests/test_gpu_fuzz.py: every fuzz test over fresh seeds until a time budget runs out,
 printing a progress line per round.  Stops at the first mismatch (the seed is in the message).
-    python tools/fuzz_soak.py [seconds] [first_seed]"""
+    python tools/fuzz_soak.py [seconds] [first_seed] [batcher]"""
 import os
 import sys
 import time
@@ -13,16 +13,26 @@ import torch  # noqa: E402
 
 import brb_framework_amd as brb  # noqa: E402
 import oracle  # noqa: E402
+import test_batcher as B  # noqa: E402
 import test_gpu_fuzz as F  # noqa: E402
 
 budget = float(sys.argv[1]) if len(sys.argv) > 1 else 240.0
 seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+batcher = len(sys.argv) > 3 and sys.argv[3] == "batcher"     # the event loop of test_batcher.py instead
 brb.lib()
 oracle.lib()
 assert torch.cuda.is_available() and brb.gpu_available()
 t0 = time.time()
 cases = 0
-while time.time() - t0 < budget:
+while batcher and time.time() - t0 < budget:
+    for algo in (1, 2):
+        for zc in (False, True):
+            for pl in (False, True):
+                B._event_loop(brb, oracle, algo, zc, pl, seed=seed, rounds=4)
+    cases += 8
+    print(f"batcher seed {seed} ok  ({cases} event loops of 4 rounds, {time.time() - t0:.0f} s)", flush=True)
+    seed += 1
+while not batcher and time.time() - t0 < budget:
     F.test_fuzz_fixed_stride(brb, oracle, torch, seed)
     F.test_fuzz_variable_length(brb, oracle, torch, seed)
     for sl in (0, 1, 2):
@@ -35,4 +45,4 @@ while time.time() - t0 < budget:
     cases += 10
     print(f"seed {seed} ok  ({cases} cases, {time.time() - t0:.0f} s)", flush=True)
     seed += 1
-print(f"soak: {cases} cases over seeds up to {seed - 1}, no mismatch", flush=True)
+print(f"soak{' (batcher)' if batcher else ''}: {cases} cases over seeds up to {seed - 1}, no mismatch", flush=True)
