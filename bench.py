@@ -426,8 +426,15 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
         # after the cfg5 leg or on a fresh box the first K = 20 launches ran 22.1 us against 20.5 us
         # settled (tools/gpu_short_bench.sh, profiles/r05/short/).  Untimed, like the W steps; the
         # timed region is still exactly K steps.  Recorded on the line as "settle".
-        t0, chunk, m = time.perf_counter(), 4, 0
+        # With several ranks the settle ends together on all of them, so that no GPU idles at the
+        # region's barrier waiting for a slower rank (an idle spell is what the settle is against):
+        # the timed part (chunks of <= 20 ms, so ranks leave it within one chunk) is followed by a
+        # collective that agrees the launch time, then ~50 ms of the same number of launches on
+        # every rank.
         settle_s = getattr(args, "settle_s", warm_s)
+        if settle_s > 0:
+            max_over_ranks(0.0)                     # a collective: the ranks start the settle together
+        t0, chunk, m, dt = time.perf_counter(), 4, 0, None
         while time.perf_counter() - t0 < settle_s:
             tc = time.perf_counter()
             for _ in range(chunk):
@@ -435,7 +442,13 @@ def warm_up(args, launch, streams, torch, max_over_ranks, warm_s=1.0, timed_s=0.
                 m += 1
             torch.cuda.synchronize()
             dt = (time.perf_counter() - tc) / chunk
-            chunk = min(chunk * 2, max(4, int(0.1 / max(dt, 1e-7))))
+            chunk = min(chunk * 2, max(4, int(0.02 / max(dt, 1e-7))))
+        if dt is not None:
+            tail = max(4, math.ceil(0.05 / max(max_over_ranks(dt), 1e-7)))
+            for _ in range(tail):
+                launch(m, streams[m % len(streams)], m % len(streams))
+                m += 1
+            torch.cuda.synchronize()
         SETTLE = None if m == 0 else {"launches": m, "seconds": round(time.perf_counter() - t0, 3),
                   "why": "untimed launches of the same step before the W warm-up steps, so the timed region "
                          "starts at the clock the chip holds under this load (a short W does not reach it)"}
