@@ -416,7 +416,9 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * pass and RC4+MD5 frame / open wave pairs get a protocol fault injected, so the call returns
  * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped), "line_pool" -1/0/k
  * (fixed-stride line digests of large batches: the launcher's default number of group rounds left to
- * the chip-wide tail pool / no pool / k rounds).  Returns 1 and the previous
+ * the chip-wide tail pool / no pool / k rounds), "line_lock" -1/0/k (fixed-stride line digests of
+ * large batches: the launcher's default / tickets / a static split whose SIMD partners are kept in
+ * lockstep, k = lead | slack << 4).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */
