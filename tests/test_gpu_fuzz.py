@@ -7,11 +7,19 @@ so the whole file runs in well under a minute on one MI355X; the fixed seeds mak
 reproducible.  SURVEY §7 edge cases; the reference has no tests of its own for this path (§4).
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+# batch sizes scale with BRB_FUZZ_SCALE (tools/fuzz_soak.py --scale; 1 in the suite)
+SCALE = max(1, int(os.environ.get("BRB_FUZZ_SCALE", "1")))
+
+
+def _n(hi):
+    return hi * SCALE
 
 
 @pytest.fixture(scope="module")
@@ -62,7 +70,7 @@ def test_fuzz_fixed_stride(brb, orc, torch_dev, seed):
         pick = rng.integers(0, 4)
         rec_len = int([rng.integers(1, 130), rng.integers(130, 3100), rng.integers(3100, 9000),
                        rng.choice([63, 64, 65, 127, 128, 129, 1500, 2048])][pick])
-        n = int(rng.integers(1, 3000 if rec_len < 3100 else 400))
+        n = int(rng.integers(1, _n(3000) if rec_len < 3100 else _n(400)))
         shift = int(rng.integers(0, 64))
         data = rng.integers(0, 256, shift + rec_len * n + 64, dtype=np.uint8)
         d = _dev(torch_dev, data)
@@ -80,7 +88,7 @@ def test_fuzz_variable_length(brb, orc, torch_dev, seed):
     with gaps or overlapping."""
     rng = np.random.default_rng(0xF2C5 + seed)
     for case in range(4):
-        n = int(rng.integers(1, 2500))
+        n = int(rng.integers(1, _n(2500)))
         lens = _lengths(rng, n)
         offs, size = _layout(rng, lens, overlap=bool(case & 1))
         data = rng.integers(0, 256, size, dtype=np.uint8)
@@ -98,7 +106,7 @@ def test_fuzz_segments(brb, torch_dev, seed, seg_line):
     (overlapping), under each kernel form (seg_line 0 per-lane, 1 line-staged, 2 wave pairs)."""
     rng = np.random.default_rng(0xF3C5 + 16 * seed + seg_line)
     for _ in range(3):
-        n = int(rng.integers(1, 1200))
+        n = int(rng.integers(1, _n(1200)))
         k = rng.integers(0, 8, n)
         k[0] = max(int(k[0]), 1)                  # at least one segment in the call
         first = np.concatenate([[0], np.cumsum(k)]).astype(np.uint64)
@@ -122,7 +130,7 @@ def test_fuzz_rc4(brb, orc, torch_dev, seed):
     """BRB_RC4_CryptBatch in place: mixed stream lengths at any byte offset, two passes so the
     states carry; ciphertext and states against the oracle."""
     rng = np.random.default_rng(0xF4C5 + seed)
-    n = int(rng.integers(1, 1500))
+    n = int(rng.integers(1, _n(1500)))
     lens = _lengths(rng, n, hi=3000)
     offs, size = _layout(rng, lens, overlap=False)
     data = rng.integers(0, 256, size, dtype=np.uint8)
@@ -143,7 +151,7 @@ def test_fuzz_base64(brb, orc, torch_dev, seed):
     """BRB_Base64EncodeBatch / DecodeBatch: mixed lengths (0 included) at any offset; the text against
     the oracle's encoder; decoded back as the reference decodes (each "=" a zero byte)."""
     rng = np.random.default_rng(0xF5C5 + seed)
-    n = int(rng.integers(1, 400))
+    n = int(rng.integers(1, _n(400)))
     lens = _lengths(rng, n, hi=2500)
     offs, size = _layout(rng, lens, overlap=False)
     data = rng.integers(0, 256, size, dtype=np.uint8)
@@ -182,7 +190,7 @@ def test_fuzz_blowfish(brb, orc, torch_dev, seed):
     rng = np.random.default_rng(0xF6C5 + seed)
     key = rng.integers(0, 256, int(rng.integers(1, 57)), dtype=np.uint8).tobytes()
     ctx = brb.blowfish_init(key)
-    n = int(rng.integers(1, 200000))
+    n = int(rng.integers(1, _n(200000)))
     words = rng.integers(0, 2**63, 2 * n, dtype=np.int64) * np.int64(1 + (seed & 1))
     w = _dev(torch_dev, words)
     brb.blowfish_encrypt_batch(ctx, w, n_blocks=n)
@@ -199,7 +207,7 @@ def test_fuzz_rc4md5_frame_open(brb, orc, torch_dev, seed):
     (one byte flipped) so their validation result is the oracle's (a flip inside the salt passes)."""
     rng = np.random.default_rng(0xF7C5 + seed)
     H = brb.RC4MD5_HEADER
-    n = int(rng.integers(1, 1200))
+    n = int(rng.integers(1, _n(1200)))
     lens = _lengths(rng, n, hi=3000)
     offs, size = _layout(rng, lens, overlap=False)
     payload = rng.integers(0, 256, size, dtype=np.uint8)
@@ -244,7 +252,7 @@ def test_fuzz_host_mode(brb, orc, torch_dev, seed):
     """The same shapes through host mode (numpy in and out: the library stages the records, runs the
     kernels and copies the results back): fixed and variable-length digests, segments, RC4."""
     rng = np.random.default_rng(0xF8C5 + seed)
-    n = int(rng.integers(1, 2000))
+    n = int(rng.integers(1, _n(2000)))
     lens = _lengths(rng, n)
     offs, size = _layout(rng, lens, overlap=bool(seed & 1))
     data = rng.integers(0, 256, size, dtype=np.uint8)

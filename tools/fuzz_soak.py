@@ -1,6 +1,6 @@
 """Soak run of tests/test_gpu_fuzz.py: every fuzz test over fresh seeds until a time budget runs out,
 printing a progress line per round.  Stops at the first mismatch (the seed is in the message).
-    python tools/fuzz_soak.py [seconds] [first_seed] [batcher]"""
+    python tools/fuzz_soak.py [--scale=k] [seconds] [first_seed] [batcher]"""
 import os
 import sys
 import time
@@ -8,6 +8,11 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+for a in list(sys.argv[1:]):                  # --scale k: batch sizes x k (BRB_FUZZ_SCALE)
+    if a.startswith("--scale="):
+        os.environ["BRB_FUZZ_SCALE"] = a.split("=", 1)[1]
+        sys.argv.remove(a)
 
 import torch  # noqa: E402
 
