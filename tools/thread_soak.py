@@ -2,7 +2,7 @@
 on its own HIP stream (device mode, sync and async) or through host mode, and check every result
 against oracle digests computed up front.  The library keeps per-thread workspaces, pipes and fault
 words; this is the many-threads shape of a receive loop's workers.
-    python tools/thread_soak.py [seconds] [threads]"""
+    python tools/thread_soak.py [--devices=k] [seconds] [threads]"""
 import os
 import sys
 import threading
@@ -17,9 +17,16 @@ import torch  # noqa: E402
 import brb_framework_amd as brb  # noqa: E402
 import oracle  # noqa: E402
 
+parts = 0
+for a in list(sys.argv[1:]):                  # --devices=k: add all-devices calls forced into k parts
+    if a.startswith("--devices="):
+        parts = int(a.split("=", 1)[1])
+        sys.argv.remove(a)
 budget = float(sys.argv[1]) if len(sys.argv) > 1 else 120.0
 nthreads = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 assert torch.cuda.is_available() and brb.gpu_available()
+if parts:
+    brb.test_option("devices", parts)
 rng = np.random.default_rng(0x50AC)
 sets = []
 for i in range(6):                                   # (data, offsets, lengths, md5, sha1) per set
@@ -46,7 +53,7 @@ def worker(t):
     ctx = brb.blowfish_init(bf_key)
     try:
         while time.time() < stop and not errors:
-            kind = int(r.integers(0, 6))
+            kind = int(r.integers(0, 8 if parts else 6))
             i = int(r.integers(0, len(sets)))
             data, offs, lens, want5, want1 = sets[i]
             if kind == 0:                            # host mode
@@ -70,8 +77,14 @@ def worker(t):
                 brb.blowfish_encrypt_batch(ctx, w)
                 brb.blowfish_decrypt_batch(ctx, w)
                 assert np.array_equal(w, bf_words), ("blowfish", t)
-            else:                                    # host-mode fixed stride
+            elif kind == 5:                          # host-mode fixed stride
                 assert np.array_equal(brb.md5_batch_fixed(fixed, 1500, 30000), fixed_md5), ("host fixed", t)
+            elif kind == 6:                          # all-devices split (forced parts)
+                got = brb.md5_batch(data, offs, lens, all_devices=True)
+                assert np.array_equal(got, want5), ("all-devices md5", t, i)
+            else:
+                got = brb.md5_batch_fixed(fixed, 1500, 30000, all_devices=True)
+                assert np.array_equal(got, fixed_md5), ("all-devices fixed", t)
             counts[t] += 1
     except Exception as e:                           # noqa: BLE001 -- reported below, ends the soak
         errors.append(repr(e))
