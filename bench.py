@@ -164,7 +164,7 @@ def core_counts(threads: int, single_core_rate: float) -> dict:
 def kernel_id(name: str) -> str:
     """A rocprofv3 kernel name without `void`, namespaces and the argument list: the kernel and its
     template arguments, e.g. "rc4_crypt_pair_kernel<false>", "digest_line_kernel<Md5Alg, 8, true,
-    true, true>".  tools/collect_profiles.py records these in pmc_traffic.json."""
+    true>".  tools/collect_profiles.py records these in pmc_traffic.json."""
     n = name.strip()
     if n.startswith("void "):
         n = n[5:]
@@ -188,8 +188,9 @@ def timed_kernel_patterns(key, opt):
     seg = opt("seg_line")
     rc4_pair = opt("rc4_pair") != 0 and opt("rc4_sector") < 0
     table = {
-        "cfg2_md5": [r"digest_line_kernel<Md5Alg, .*>"],
-        "cfg2_sha1": [r"digest_line_kernel<Sha1Alg, .*>"],
+        # <Alg, waves, output 16-aligned, TAIL_HI>: the only forms launch_fixed_line launches
+        "cfg2_md5": [r"digest_line_kernel<Md5Alg, 8, (true|false), (true|false)>"],
+        "cfg2_sha1": [r"digest_line_kernel<Sha1Alg, 8, (true|false), (true|false)>"],
         "cfg3_md5": [r"digest_b64r_kernel<Md5Alg, .*>"],
         "cfg4_blowfish": [r"bf_rep_kernel<\d+, false>", r"bf_rep_kernel<\d+, true>"],
         "f1_rc4": [r"rc4_crypt_pair_kernel<false>"] if rc4_pair else [r"rc4_crypt_kernel<(true|false)>"],
@@ -515,23 +516,25 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
         e.record(streams[0])
     gc_was = gc.isenabled()
     gc.disable()         # no collector pause inside a region of a few hundred microseconds
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if steady:
-        ea.record(streams[0])
-    else:
-        e0.record(streams[0])
-    for k in range(n_steps):
-        j = k % len(streams)
-        launch(k, streams[j], j)
-        if steady and k == 1:
+    try:                 # a raise inside the region must not leave the collector off
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if steady:
+            ea.record(streams[0])
+        else:
             e0.record(streams[0])
-    e1.record(streams[0])
-    torch.cuda.synchronize()
-    barrier()
-    if gc_was:
-        gc.enable()
+        for k in range(n_steps):
+            j = k % len(streams)
+            launch(k, streams[j], j)
+            if steady and k == 1:
+                e0.record(streams[0])
+        e1.record(streams[0])
+        torch.cuda.synchronize()
+        barrier()
+    finally:
+        if gc_was:
+            gc.enable()
     if MARK:             # sentinel after the region, enqueued after the timing ended
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)

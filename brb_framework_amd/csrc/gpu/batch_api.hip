@@ -105,6 +105,10 @@ struct Workspaces {
     std::vector<std::pair<void *, size_t>> by_dev;   // (ptr, capacity) per device ordinal
     uint32_t *fault_word = nullptr;                   // pair_fault.h: the thread's fault word
     uint32_t *async_word = nullptr;                   // ... and its sticky word for ASYNC calls
+    // Devices on which a device-mode ASYNC call armed async_word (bit d; bit 63 also stands for every
+    // device >= 63).  Those calls return before their kernels run, so a pair kernel may still write
+    // the word after the thread cleans up: release() first drains these devices.
+    uint64_t async_devs = 0;
     void release()
     {
         for (size_t d = 0; d < by_dev.size(); d++)
@@ -113,6 +117,19 @@ struct Workspaces {
                 (void)hipFree(by_dev[d].first);
                 by_dev[d] = {nullptr, 0};
             }
+        if (async_word && async_devs) {
+            int n = 0;
+            if (hipGetDeviceCount(&n) != hipSuccess)
+                n = 0;
+            for (int d = 0; d < n; d++)
+                if (async_devs & (uint64_t(1) << (d < 63 ? d : 63))) {
+                    brb_api::DeviceGuard g{d};
+                    if (g.error() == hipSuccess)
+                        (void)hipDeviceSynchronize();
+                }
+            (void)hipGetLastError();
+            async_devs = 0;
+        }
         for (uint32_t **w : {&fault_word, &async_word})
             if (*w) {
                 (void)hipHostFree(*w);
@@ -154,6 +171,9 @@ struct PairFault {
     {
         if ((flags & BRB_BATCH_DEVICE) && (flags & BRB_BATCH_ASYNC)) {
             t_fault_armed = alloc_fault_word(&t_ws.async_word);
+            int dev = 0;
+            if (t_fault_armed && hipGetDevice(&dev) == hipSuccess && dev >= 0)
+                t_ws.async_devs |= uint64_t(1) << (dev < 63 ? dev : 63);
             return;
         }
         w = fault_word();
@@ -177,7 +197,9 @@ struct PairFault {
 
 void release_thread_resources()
 {
-    if (device_count() > 0) {   // host-mode calls have drained their streams before returning
+    // host-mode calls have drained their streams before returning; device-mode ASYNC calls may not
+    // have, and release() drains the devices they armed the async fault word on before freeing it
+    if (device_count() > 0) {
         t_ws.release();
         brb_host::release_thread_pipes();
     }
@@ -1107,9 +1129,7 @@ extern "C" int BRB_CryptoGPU_TestOption(const char *name, int value, int *old)
                  {"line_slots", brb_opt::kLineSlots, 0, 3},
                  {"rc4md5_pair", brb_opt::kRc4Pair, 0, 1},
                  {"rc4_pair", brb_opt::kRc4CryptPair, 0, 1},
-                 {"pair_stall", brb_opt::kPairStall, 0, 1},
-                 {"line_pool", brb_opt::kLinePool, -1, 64},
-                 {"line_lock", brb_opt::kLineLock, -1, 255}};
+                 {"pair_stall", brb_opt::kPairStall, 0, 1}};
     if (!name) {
         set_err("NULL option name");
         return BRB_BATCH_BADARG;

@@ -28,15 +28,10 @@ enum Opt {
     kPairStall = 13,    // 1: inject a protocol fault into the segment-digest, MetaData, RC4-pass and frame/open wave pairs
                         // (the first workgroup's first pair never hands over its first plan / block), so the
                         // tests see a bounded wait give up and the call report it (pair_fault.h); 0: off
-    kLinePool = 14,     // fixed-stride line digests: rounds of groups left to the chip-wide tail pool
-                        // (digest_line.h POOL); -1 the launcher's default, 0 no pool
-    kLineLock = 15,     // fixed-stride line digests of large batches: k >= 1 a static split whose SIMD partners
-                        // progress in lockstep, the first (k & 15) iterations ahead, priorities set only past
-                        // a drift of k >> 4 iterations (digest_line.h LOCK); 0 tickets (DYN); -1 the default
-    kCount = 16
+    kCount = 14
 };
 
-inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0, -1, -1};
+inline std::atomic<int> g_opt[kCount] = {-1, 1, 1, 1, 0, -1, 0, 0, 2, 2, 0, 1, 1, 0};
 
 inline int get(Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
 

@@ -50,6 +50,7 @@ struct Item {
     uint32_t out_len;
     uint64_t salt;
     uint32_t round;   // sub-round
+    uint32_t epoch;   // the connection's key epoch at submission (BRB_TransformBatcher::epoch)
 };
 
 // Page-locked host ranges registered through BRB_CryptoGPU_HostRegister: host base, length, the
@@ -229,6 +230,14 @@ struct BRB_TransformBatcher {
     uint64_t max_items = 0;    // buffers per round: 4 per connection on average
     Round r[2];
     std::vector<uint8_t> enabled;
+    // Key epochs: Enable starts a connection's next epoch; a round dropped for a device
+    // fault leaves the states of its connections out of step, so their epoch is poisoned
+    // (poison_upto[c] = the last poisoned epoch).  A buffer of a poisoned epoch is never delivered as
+    // data: one already launched behind the faulted round (pipelined FlushAsync) comes back
+    // BRB_TRANSFORM_DROPPED, one still waiting in the filling round is dropped without running, and
+    // Read/Write refuse the connection until Enable re-keys it.  Atomics: submitting threads read
+    // them while a Flush on another thread poisons.
+    std::vector<uint32_t> epoch, poison_upto;
     // BRB_BATCHER_ALL_DEVICES: the connections are partitioned over G sub-batchers, connection c
     // in sub c % G as its connection c / G, sub g on device g % (visible devices); this object then
     // only routes (no collective -- a connection's states live on its device).
@@ -335,6 +344,8 @@ BRB_TransformBatcher *BRB_TransformBatcherCreate(uint32_t max_conns, uint64_t ma
     b->zc = zc;
     b->n_rounds = pipelined ? 2 : 1;
     b->enabled.assign(max_conns, 0);
+    b->epoch.assign(max_conns, 0);
+    b->poison_upto.assign(max_conns, 0);
     // outputs: every buffer may grow by a frame header; metadata: per item and sub-round arrays
     b->max_items = 4 * uint64_t(max_conns);
     b->out_cap = up(max_round_bytes + kHdr * b->max_items, kAlign);
@@ -394,6 +405,7 @@ int BRB_TransformBatcherEnable(BRB_TransformBatcher *b, uint32_t conn, const voi
     if ((e = hipStreamSynchronize(b->stream)) != hipSuccess)
         return fail_hip("hipStreamSynchronize", e);
     b->enabled[conn] = 1;
+    __atomic_fetch_add(&b->epoch[conn], 1u, __ATOMIC_RELEASE);   // buffers from here on: the fresh key
     return BRB_BATCH_OK;
 }
 
@@ -404,6 +416,12 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
         return submit(b->subs[conn % b->subs.size()], conn / uint32_t(b->subs.size()), op, data, len, salt);
     if (!b || (!data && len) || conn >= b->max_conns || !b->enabled[conn]) {
         set_err("bad batcher, data or connection (not enabled?)");
+        return BRB_BATCH_BADARG;
+    }
+    const uint32_t ep = __atomic_load_n(&b->epoch[conn], __ATOMIC_ACQUIRE);
+    if (ep <= __atomic_load_n(&b->poison_upto[conn], __ATOMIC_ACQUIRE)) {
+        set_err("connection %u: its RC4 states are out of step after a round dropped for a device fault; re-key it "
+                "with Enable", conn);
         return BRB_BATCH_BADARG;
     }
     Round &R = b->r[b->cur];
@@ -447,7 +465,7 @@ static int submit(BRB_TransformBatcher *b, uint32_t conn, int op, const void *da
     }
     Item &it = R.slots[k.slot];
     const uint64_t in_off = k.in, out_off = k.out;
-    it = Item{conn, op, in_off, len, out_off, out_len, salt, 0};
+    it = Item{conn, op, in_off, len, out_off, out_len, salt, 0, ep};
     if (b->zc) {
         uintptr_t d = 0;
         if (len && !host_to_device(data, len, &d, b->dev)) {
@@ -477,14 +495,32 @@ int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void
 
 }  // extern "C"
 
+// A buffer of a poisoned key epoch (its connection's states went out of step in a dropped round).
+static bool poisoned(const BRB_TransformBatcher *b, const Item &it)
+{
+    return it.epoch <= __atomic_load_n(&b->poison_upto[it.conn], __ATOMIC_ACQUIRE);
+}
+
+// A round dropped for a device fault: every connection it holds is poisoned up to the epoch its
+// buffers were submitted under (a later Enable has already started a fresh one).
+static void poison_round(BRB_TransformBatcher *b, const Round &R)
+{
+    for (const Item &it : R.items)
+        if (__atomic_load_n(&b->poison_upto[it.conn], __ATOMIC_RELAXED) < it.epoch)
+            __atomic_store_n(&b->poison_upto[it.conn], it.epoch, __ATOMIC_RELEASE);
+}
+
 // The round's buffers in slot order, holes dropped.  Called once no Read/Write is running on R.
-static size_t collect(BRB_TransformBatcher *b, Round &R)
+// Buffers of poisoned epochs (submitted before a fault was found) go to *stale instead: they must
+// not run, since they would advance the states an Enable re-keys.
+static size_t collect(BRB_TransformBatcher *b, Round &R, std::vector<Item> *stale)
 {
     const uint64_t n = std::min<uint64_t>(R.n_slots, b->max_items);
     R.items.clear();
+    stale->clear();
     for (uint64_t i = 0; i < n; i++)
         if (R.slots[i].conn != kHole)
-            R.items.push_back(R.slots[i]);
+            (poisoned(b, R.slots[i]) ? *stale : R.items).push_back(R.slots[i]);
     return R.items.size();
 }
 
@@ -659,14 +695,19 @@ static int launch_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone don
 
 // Waits for round R and hands every result back in submission order; the k-th read item of a
 // group has valid flag k of that group.  Returns the number of buffers delivered, or -1 when the
-// round failed on the device (dropped: drop_round's callbacks; reason in LastError).
-static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user)
+// round failed on the device (dropped: drop_round's callbacks, its connections poisoned; reason in
+// LastError).  Buffers of connections poisoned after R was launched come back
+// BRB_TRANSFORM_DROPPED and are counted in *n_stale.
+static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDone done, void *user, int64_t *n_stale)
 {
     hipError_t e;
+    *n_stale = 0;
     if ((e = hipEventSynchronize(R.done)) != hipSuccess) {
         fail_hip("round completion", e);
         const std::string why = brb_api::t_err;
-        set_err("%s; round of %zu buffers dropped", why.c_str(), R.items.size());
+        set_err("%s; round of %zu buffers dropped (its connections' states are out of step: re-key them with Enable)",
+                why.c_str(), R.items.size());
+        poison_round(b, R);
         drop_round(R, done, user);
         return -1;
     }
@@ -677,13 +718,22 @@ static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDon
         set_err("wave-pair protocol fault: a kernel of the round gave up waiting on its partner wave; round of %zu "
                 "buffers dropped (its connections' states are out of step: re-key them with Enable)",
                 R.items.size());
+        poison_round(b, R);
         drop_round(R, done, user);
         return -1;
     }
     std::vector<uint32_t> next_in_group(R.group_valid.size(), 0);
+    int64_t delivered = 0;
     for (const Item &it : R.items) {
         const int64_t gi = R.group_of[size_t(it.round) * 2 + it.op];
         const uint32_t k = next_in_group[gi]++;
+        if (poisoned(b, it)) {          // ran on states a faulted round before it left out of step
+            ++*n_stale;
+            if (done)
+                done(user, it.conn, it.op, nullptr, 0, BRB_TRANSFORM_DROPPED);
+            continue;
+        }
+        ++delivered;
         int valid = 1;
         const uint8_t *out;
         if (b->zc) {
@@ -701,9 +751,11 @@ static int64_t deliver_round(BRB_TransformBatcher *b, Round &R, BRB_TransformDon
         if (done)
             done(user, it.conn, it.op, out, it.out_len, valid);
     }
-    const int64_t n = int64_t(R.items.size());
+    if (*n_stale)
+        set_err("%lld buffers of connections whose states a faulted round left out of step were dropped (re-key "
+                "them with Enable)", (long long)*n_stale);
     R.reset();
-    return n;
+    return delivered;
 }
 
 // ---- Flush / FlushAsync in phases, so that an all-devices batcher can enqueue every device's
@@ -718,6 +770,7 @@ struct Phase {
     void *user;
     Round *prev = nullptr;     // FlushAsync: the round to deliver after the launches
     int64_t n = 0;             // buffers delivered
+    std::vector<Item> stale;   // the launched round's buffers of poisoned epochs (phase_stale)
     bool dropped = false;
     bool failed = false;       // hipSetDevice failed: the round stays pending
 };
@@ -744,10 +797,11 @@ static void phase_deliver(Phase &p, Round &R)
         p.failed = true;
         return;
     }
-    const int64_t n = deliver_round(p.b, R, p.done, p.user);
-    if (n < 0)
+    int64_t stale = 0;
+    const int64_t n = deliver_round(p.b, R, p.done, p.user, &stale);
+    if (n < 0 || stale)
         p.dropped = true;
-    else
+    if (n > 0)
         p.n += n;
 }
 
@@ -762,12 +816,29 @@ static void phase_launch(Phase &p, bool async)
     }
     Round &R = b->r[b->cur];
     p.prev = async && b->n_rounds == 2 ? &b->r[b->cur ^ 1] : nullptr;
-    if (collect(b, R) == 0)
+    const size_t n = collect(b, R, &p.stale);
+    if (n == 0)
         R.reset();
     else if (launch_round(b, R, p.done, p.user) != BRB_BATCH_OK)   // dropped: its callbacks have fired
         p.dropped = true;
     if (async && b->n_rounds == 2 && R.in_flight)
         b->cur ^= 1;        // Read/Write now fill the other arena (the previous round's, once delivered)
+}
+
+// The buffers phase_launch left out (submitted under a poisoned epoch, never run): their callbacks
+// fire after the round before theirs was delivered and before their own round's results, so every
+// connection still sees its buffers in submission order.
+static void phase_stale(Phase &p)
+{
+    if (p.stale.empty())
+        return;
+    if (p.done)
+        for (const Item &it : p.stale)
+            p.done(p.user, it.conn, it.op, nullptr, 0, BRB_TRANSFORM_DROPPED);
+    set_err("%zu buffers of connections whose states a faulted round left out of step were dropped without running "
+            "(re-key them with Enable)", p.stale.size());
+    p.dropped = true;
+    p.stale.clear();
 }
 
 static int64_t flush_all(BRB_TransformBatcher *b, BRB_TransformDone done, void *user, bool async)
@@ -790,14 +861,18 @@ static int64_t flush_all(BRB_TransformBatcher *b, BRB_TransformDone done, void *
                 phase_deliver(p, p.b->r[p.b->cur ^ 1]);
         for (Phase &p : ph)
             phase_launch(p, false);
-        for (Phase &p : ph)
+        for (Phase &p : ph) {
+            phase_stale(p);
             phase_deliver(p, p.b->r[p.b->cur]);
+        }
     } else {
         for (Phase &p : ph)
             phase_launch(p, true);
-        for (Phase &p : ph)
+        for (Phase &p : ph) {
             if (p.prev)
                 phase_deliver(p, *p.prev);
+            phase_stale(p);
+        }
     }
     int64_t total = 0;
     bool dropped = false;

@@ -315,8 +315,14 @@ int BRB_TransformBatcherWrite(BRB_TransformBatcher *b, uint32_t conn, const void
  * another round was delivered in the same call, whose buffers came back through their callbacks as
  * usual (and BRB_BATCH_PARTIAL when, besides, a part's round stays pending).  A round in which a
  * wave-pair kernel reports a protocol fault (BRB_BATCH_FAULT above) is dropped the same way, so no
- * output, frame or valid flag computed over wrong bytes is ever delivered.  Such connections are out of step with their peers, as after a lost buffer in the
- * reference, and are re-keyed with Enable.  On a pipelined batcher Flush first delivers the round
+ * output, frame or valid flag computed over wrong bytes is ever delivered.  The connections of a round
+ * dropped on the device (a completion error or a wave-pair fault) are out of step with their peers, as
+ * after a lost buffer in the reference, and stay poisoned until Enable re-keys them: their buffers
+ * already launched behind the dropped round (pipelined FlushAsync) and those still waiting in the
+ * filling round come back BRB_TRANSFORM_DROPPED (the call returns BRB_BATCH_DROPPED), and Read/Write
+ * refuse them (BRB_BATCH_BADARG) until then.  A round whose kernel launch failed on the host is
+ * dropped without poisoning (only the groups launched before the failure ran, once each).  On a
+ * pipelined batcher Flush first delivers the round
  * FlushAsync left running, so Flush drains everything.  A batcher's calls run on the device it was
  * created on and leave the calling thread's current device unchanged. */
 int64_t BRB_TransformBatcherFlush(BRB_TransformBatcher *b, BRB_TransformDone done, void *user);
@@ -383,7 +389,9 @@ int BRB_CryptoGPU_SetDevice(int dev);
 /* The calling thread's current device, or -1 (reason in LastError). */
 int BRB_CryptoGPU_GetDevice(void);
 /* Frees the calling thread's host-mode scratch (device workspaces, streams, events) now instead of
- * at thread exit.  Call it with no batch call of this thread running. */
+ * at thread exit.  Call it with no batch call of this thread running.  If the thread made
+ * device-mode BRB_BATCH_ASYNC calls of wave-pair kernels, their devices are synchronised first
+ * (hipDeviceSynchronize), since those kernels may still write the thread's fault word. */
 void BRB_CryptoGPU_ThreadCleanup(void);
 /* Last error of the calling thread ("" if none). */
 const char *BRB_CryptoGPU_LastError(void);
@@ -414,11 +422,7 @@ int BRB_CryptoGPU_HostUnregister(void *p);
  * partner wave pairs / one wave per connection), "rc4_pair" 1/0 (BRB_RC4_CryptBatch likewise; a forced
  * "rc4_sector" value selects the one-wave kernel), "pair_stall" 0/1 (1: the segment, MetaData, RC4
  * pass and RC4+MD5 frame / open wave pairs get a protocol fault injected, so the call returns
- * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped), "line_pool" -1/0/k
- * (fixed-stride line digests of large batches: the launcher's default number of group rounds left to
- * the chip-wide tail pool / no pool / k rounds), "line_lock" -1/0/k (fixed-stride line digests of
- * large batches: the launcher's default / tickets / a static split whose SIMD partners are kept in
- * lockstep, k = lead | slack << 4).  Returns 1 and the previous
+ * BRB_BATCH_FAULT, an async call's check reports it and a batcher round is dropped).  Returns 1 and the previous
  * value in *old (if not NULL), or -1 for an unknown name or a value out of range. */
 int BRB_CryptoGPU_TestOption(const char *name, int value, int *old);
 /* Library version string. */

@@ -154,14 +154,13 @@ def test_base64_segments_all_devices(brb, orc, torch_dev, parts):
 
 
 @pytest.mark.gpu
-def test_line_pool_forced_parts(brb, orc, torch_dev):
-    """The line kernel's tail pool (test option line_pool) under the host-mode split: three parts on
-    their worker threads, each launch taking a slot of its device's pool ring concurrently with
-    the others (300 001 records: ~100 000 per part, 7 rounds of groups, the last 2 pooled), twice."""
+def test_line_forced_parts(brb, orc, torch_dev):
+    """The line kernel under the host-mode split: three parts on their worker threads, launched
+    concurrently (300 001 records: ~100 000 per part, 7 rounds of groups, partial last groups), twice."""
     L, n = 1500, 300_001
     data = workload.gen_records(0x5EED00C4, 0, n, L)
     want = orc.md5_batch_fixed(data, L, n, threads=8)
-    with brb.TestOption("devices", 3), brb.TestOption("line_pool", 2):
+    with brb.TestOption("devices", 3):
         for _ in range(2):
             assert np.array_equal(brb.md5_batch_fixed(data, L, n, all_devices=True), want)
 

@@ -393,3 +393,85 @@ def test_pair_fault_round_dropped(brb, orc, torch_dev, algo, zero_copy, pipeline
     for c in range(0, C, 5):
         assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
     b.close()
+
+
+@pytest.mark.parametrize("how", ["async", "sync"])
+@pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("algo", [1, 2])
+def test_pipelined_fault_poisons_next_round(brb, orc, torch_dev, algo, zero_copy, how):
+    """on a pipelined batcher, round A runs with a wave-pair fault (test option
+    pair_stall) while round B is submitted behind it.  A's connections are poisoned when A is
+    dropped, so none of B's buffers on them is delivered as data -- with "async" B is launched by the
+    FlushAsync that finds A's fault (B ran on the wrong states: dropped at delivery); with "sync"
+    Flush finds the fault before launching B (B's buffers on those connections never run).
+    Connections A did not touch are delivered normally throughout.  Read/Write refuse a poisoned
+    connection until Enable re-keys it; then every connection equals the oracle again."""
+    rng = np.random.default_rng(300 + algo)
+    C, CA = 192, 160                              # round A holds connections 0..CA-1
+    keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(C)]
+    b = brb.TransformBatcher(C, 4 << 20, algo, zero_copy=zero_copy, pipelined=True)
+    st = {}
+
+    def rekey(conns):
+        for c in conns:
+            b.enable(c, keys[c])
+            st[c] = [orc.rc4_init(keys[c]) for _ in range(3)]   # ours read, ours write, peer write
+
+    def submit(c, rnd):
+        """one read and one write on connection c; returns their expected callbacks"""
+        n = int(rng.choice([0, 17, 700, 1500]))
+        payload = workload.gen_records(0x5EED00F8 + rnd, c, 1, n).tobytes() if n else b""
+        r, w, pw = st[c]
+        if algo == 2:
+            pw, frame = orc.rc4md5_frame(pw, payload, c)
+            r, dec, ok = orc.rc4md5_open(r, frame)
+            assert b.read(c, frame) == 1
+            w, out = orc.rc4md5_frame(w, payload, rnd + c)
+            exp = [(c, 0, dec, ok), (c, 1, out, 1)]
+        else:
+            pw, wire = orc.rc4_crypt(pw, payload)
+            r, dec = orc.rc4_crypt(r, wire)
+            assert b.read(c, wire) == 1
+            w, out = orc.rc4_crypt(w, payload)
+            exp = [(c, 0, dec, 1), (c, 1, out, 1)]
+        assert b.write(c, payload, rnd + c) == 1
+        st[c] = [r, w, pw]
+        return exp
+
+    def dropped(c):
+        return [(c, 0, b"", brb.TRANSFORM_DROPPED), (c, 1, b"", brb.TRANSFORM_DROPPED)]
+
+    rekey(range(C))
+    for c in range(CA):
+        submit(c, 0)
+    with brb.TestOption("rc4_pair", 1), brb.TestOption("rc4md5_pair", 1), brb.TestOption("pair_stall", 1):
+        assert b.flush_async() == []              # A launched with the stalled kernels
+    want_b = []
+    for c in range(C):                            # B: every connection, submitted before A's fault is known
+        e = submit(c, 1)
+        want_b += dropped(c) if c < CA else e
+    want_a = [x for c in range(CA) for x in dropped(c)]
+    if how == "async":
+        with pytest.raises(RuntimeError, match="wave-pair protocol fault.*dropped") as ei:
+            b.flush_async()                       # launches B, then delivers (drops) A
+        assert ei.value.code == brb.BATCH_DROPPED and ei.value.results == want_a
+        assert b.read(0, b"refused") == -1 and b.write(CA - 1, b"refused", 0) == -1
+        want_c = submit(CA, 2)                    # an untouched connection keeps working
+        with pytest.raises(RuntimeError, match="out of step.*dropped") as ei:
+            b.flush()                             # delivers B (poisoned buffers dropped), then C
+        assert ei.value.code == brb.BATCH_DROPPED
+        _check_round(ei.value.results, want_b + want_c, 1)
+    else:
+        with pytest.raises(RuntimeError, match="dropped") as ei:
+            b.flush()                             # delivers (drops) A, then runs B without its stale buffers
+        assert ei.value.code == brb.BATCH_DROPPED
+        _check_round(ei.value.results, want_a + want_b, 1)
+        assert b.read(0, b"refused") == -1
+    for c in range(CA, C, 7):                     # untouched connections: their states advanced exactly once
+        assert b.state(c, 0) == st[c][0] and b.state(c, 1) == st[c][1]
+    rekey(range(CA))                              # A's connections re-keyed, as after a lost buffer
+    want_d = [x for c in range(C) for x in submit(c, 3)]
+    _check_round(b.flush(), want_d, 3)
+    for c in range(0, C, 5):
+        assert b.state(c, 0) == st[c][0] and b.state(c, 1) == st[c][1]
+    b.close()

@@ -228,71 +228,26 @@ def test_line_kernel_short_groups(brb, orc, torch_dev, n, rec_len, off):
                           orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
-@pytest.mark.parametrize("n,rec_len,pool", [
-    (300_001, 1500, 1),      # 4 688 groups over 256 workgroups: 19 rounds, the last one pooled
-    (300_001, 260, 8),       # K = 3, 8 of 19 rounds pooled, a partial last group
-    (70_000, 68, 2),         # K = 1: the pool ticket is taken at the last (only) iteration
-    (70_000, 196, 2),        # K = 2: the ticket requested in iteration 1, iteration 2 the last
-    (300_001, 260, 4),       # K = 3: iterations 1 and 2 full, the loop below starts at k = 3
-    (300_001, 388, 4),       # K = 4
-    (1 << 20, 1500, 32),     # the cfg5 shard, half of it pooled
-    (1 << 20, 1500, 0),      # ... and without the pool
+@pytest.mark.parametrize("rec_len,off", [
+    (68, 4), (128, 8), (132, 12), (192, 0), (196, 4), (256, 8), (260, 12), (320, 0),
+    (1024, 4), (1476, 8), (1500, 12), (1532, 0), (1540, 4),
 ])
-def test_line_pool_tail(brb, orc, torch_dev, n, rec_len, pool):
-    """The line kernel's chip-wide tail pool (digest_line.h POOL, test option line_pool = rounds
-    pooled): every digest against the oracle, three launches back to back (each launch's last
-    workgroup zeroes the heads its slot's next user starts from)."""
-    data = workload.gen_records(0x5EED0015, 0, n, rec_len)
-    d = to_dev(torch_dev, data)
+def test_line_kernel_parities(brb, orc, torch_dev, rec_len, off):
+    """The line kernel's launch-uniform choices (digest_line.h, round 6): K odd and even (slot P of a
+    group's line 0), the tail in the last iteration's first or second block (TAIL_HI), no tail
+    (t = 0), with the per-wave window and DMA tables shared by every group -- several groups per
+    wave, a partial last group (300 001 records), buffer offsets 0/4/8/12, MD5 and SHA-1 against
+    the oracle, two launches back to back."""
+    n = 300_001
+    data = workload.gen_records(0x5EED0015 ^ rec_len, 0, n, rec_len)
+    d = torch_dev.zeros(data.size + 64, dtype=torch_dev.uint8, device="cuda")
+    d[off:off + data.size] = to_dev(torch_dev, data)
+    view = d[off:off + data.size]
     want = orc.md5_batch_fixed(data, rec_len, n, threads=16)
-    with brb.TestOption("line_pool", pool):
-        for _ in range(3):
-            assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want)
-        assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),
-                              orc.sha1_batch_fixed(data, rec_len, n, threads=16))
-
-
-@pytest.mark.parametrize("n,rec_len", [
-    (1 << 20, 1500),         # the cfg5 shard: 8 groups per wave exactly
-    (300_001, 260),          # K = 3, 4 688 groups over 2 048 waves (2 or 3 each), a partial last group
-    (1 << 20, 68),           # K = 1
-    (300_001, 196),          # K = 2
-])
-@pytest.mark.parametrize("lead", [1, 4])
-def test_line_lock(brb, orc, torch_dev, n, rec_len, lead):
-    """The static split with SIMD partners in lockstep, the first `lead` iterations ahead
-    (digest_line.h LOCK, test option line_lock = lead): every digest against the oracle, MD5 and
-    SHA-1, two launches back to back."""
-    data = workload.gen_records(0x5EED0017, 0, n, rec_len)
-    d = to_dev(torch_dev, data)
-    want = orc.md5_batch_fixed(data, rec_len, n, threads=16)
-    with brb.TestOption("line_lock", lead):
-        for _ in range(2):
-            assert np.array_equal(brb.md5_batch_fixed(d, rec_len, n).cpu().numpy(), want)
-        assert np.array_equal(brb.sha1_batch_fixed(d, rec_len, n).cpu().numpy(),
-                              orc.sha1_batch_fixed(data, rec_len, n, threads=16))
-
-
-def test_line_pool_slot_ring_wraps(brb, orc, torch_dev):
-    """More pooled launches than the ring has slots (kPoolSlots = 512), alternating over two
-    streams: every launch still equals the oracle, so every slot was left zeroed for its next user."""
-    torch = torch_dev
-    n, L = 256 * 64 * 2, 68                      # two rounds of groups: one pooled
-    data = workload.gen_records(0x5EED0016, 0, n, L)
-    d = to_dev(torch, data)
-    want = torch.from_numpy(orc.md5_batch_fixed(data, L, n, threads=16)).cuda()
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    outs = [torch.empty((n, 16), dtype=torch.uint8, device="cuda") for _ in range(8)]
-    bad = [torch.zeros((), dtype=torch.int64, device="cuda") for _ in streams]   # one per stream
-    with brb.TestOption("line_pool", 1):
-        for i in range(1100):
-            s = streams[i % 2]
-            with torch.cuda.stream(s):
-                o = outs[i % 8]
-                brb.md5_batch_fixed(d, L, n, out=o, stream=s, async_=True)
-                bad[i % 2] += (o != want).any().to(torch.int64)
-    torch.cuda.synchronize()
-    assert [int(b) for b in bad] == [0, 0]
+    for _ in range(2):
+        assert np.array_equal(brb.md5_batch_fixed(view, rec_len, n).cpu().numpy(), want)
+    assert np.array_equal(brb.sha1_batch_fixed(view, rec_len, n).cpu().numpy(),
+                          orc.sha1_batch_fixed(data, rec_len, n, threads=16))
 
 
 @pytest.mark.parametrize("rec_len", [1500, 1501])

@@ -696,3 +696,42 @@ def test_async_fault_words_are_per_thread(brb, orc, torch_dev):
     assert res["clean"] == "ok"
     with pytest.raises(RuntimeError, match="returned -4"):
         brb.async_fault_check()
+
+
+@pytest.mark.gpu
+def test_thread_cleanup_drains_async_pair_calls(brb, orc, torch_dev):
+    """a device-mode async call of a wave-pair kernel returns before the kernel runs, and
+    the kernel writes the calling thread's fault word.  A thread that cleans up (ThreadCleanup, or
+    its exit) with such a call still queued -- here behind ~0.1 s of spinning on the same stream --
+    must not free the word under the kernel: cleanup drains the devices the thread armed the word
+    on first.  The kernel's results are then the oracle's, and later calls on a fresh thread work."""
+    import threading
+    import time
+    torch = torch_dev
+    n = 128
+    offs, lens, total = _layout([4096] * n)
+    data = workload.gen_records(SEED + 13, 0, 1, total)
+    states = brb.rc4_states(_keys(n, 45))
+    ts, td = _to(torch, states), _to(torch, data)
+    to, tl = _to(torch, offs), _to(torch, lens)
+    torch.cuda.synchronize()
+    res = {}
+
+    def worker():
+        s = torch.cuda.current_stream()
+        torch.cuda._sleep(200_000_000)                     # the pair kernel queues behind this
+        with brb.TestOption("rc4_pair", 1):
+            brb.rc4_crypt_batch(ts, td, to, tl, stream=s, async_=True)
+        t0 = time.perf_counter()
+        brb.lib().BRB_CryptoGPU_ThreadCleanup()           # frees the async fault word: after the drain
+        res["cleanup_s"] = time.perf_counter() - t0
+        res["done"] = bool(torch.cuda.current_stream().query())
+
+    th = threading.Thread(target=worker)
+    th.start()
+    th.join()
+    assert res["done"], "ThreadCleanup returned with the thread's async pair kernel still queued"
+    torch.cuda.synchronize()
+    want_st, want = _oracle_crypt(orc, states, data, offs, lens)
+    assert np.array_equal(td.cpu().numpy(), want) and np.array_equal(ts.cpu().numpy(), want_st)
+    brb.async_fault_check()

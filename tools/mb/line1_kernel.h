@@ -9,6 +9,7 @@
 #pragma once
 
 #include "digest_line.h"
+#include "line_r05_kernel.h"   // round 5's line_finish / tail_masks signatures
 
 namespace brb_digest {
 
@@ -176,8 +177,8 @@ __global__ __launch_bounds__(256, 1) void digest_line1_kernel(const uint8_t *__r
         }
     }
     uint32_t tm[16], tp[16];
-    tail_masks(t, tm, tp);
-    line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, r0 + lane, n_rec);
+    brb_mb_r05::tail_masks(t, tm, tp);
+    brb_mb_r05::line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, r0 + lane, n_rec);
     BRB_LINE_PROBE(3);
 }
 

@@ -23,6 +23,7 @@
 #pragma once
 
 #include "digest_line.h"
+#include "line_r05_kernel.h"   // round 5's line_finish / tail_masks signatures
 
 namespace brb_digest {
 
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void digest_line3_kernel(const uint8
     uint64_t gn = take();
     win_setup(g);
     uint32_t tm[16], tp[16];
-    tail_masks(t, tm, tp);
+    brb_mb_r05::tail_masks(t, tm, tp);
     wait_first();
     read_window(t0, 0, w0, w1);
     wait_reads();
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void digest_line3_kernel(const uint8
         __builtin_amdgcn_sched_barrier(0);
         if (2 * K - 1 < nfull)
             Alg::compress(st, tw1);
-        line_finish<Alg, OUT_ALIGNED>(st, tw0, tw1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
+        brb_mb_r05::line_finish<Alg, OUT_ALIGNED>(st, tw0, tw1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
         if (!next)
             break;
         wait_reads();

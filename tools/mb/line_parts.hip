@@ -53,10 +53,10 @@ int main(int argc, char **argv)
     CK(hipMalloc(&o, n * 16));
     const uint64_t groups = (n + 63) / 64;
     struct V { const char *name; const void *k; int rot; int wg; int line3; };
-    V vs[] = {{"md5   HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, nrot, 8, 0},
-              {"md5   MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 1, 8, 0},
-              {"stage HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, nrot, 8, 0},
-              {"stage MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 1, 8, 0},
+    V vs[] = {{"md5   HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true>, nrot, 8, 0},
+              {"md5   MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true>, 1, 8, 0},
+              {"stage HBM (7 copies)", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true>, nrot, 8, 0},
+              {"stage MALL (1 copy) ", (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true>, 1, 8, 0},
               {"md5   HBM line3     ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, nrot, 4, 1},
               {"md5   MALL line3    ", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, true>, 1, 4, 1},
               {"md5   HBM line3 late", (const void *)(Kern)brb_digest::digest_line3_kernel<AlgLit, 4, true, false>, nrot, 4, 1},

@@ -27,6 +27,7 @@
 #pragma once
 
 #include "digest_line.h"
+#include "line_r05_kernel.h"   // round 5's line_finish / tail_masks signatures
 
 namespace brb_digest {
 
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(64 * (C + 1), 1) void digest_line_pc_kernel(const u
         }
     };
     uint32_t tm[16], tp[16];
-    tail_masks(t, tm, tp);
+    brb_mb_r05::tail_masks(t, tm, tp);
     uint32_t w0[16], w1[16];
     auto wait_ready = [&](uint32_t need) {
         uint32_t polls = 0;
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(64 * (C + 1), 1) void digest_line_pc_kernel(const u
             if (2 * K - 1 < nfull)
                 Alg::compress(st, w1);
         }
-        line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
+        brb_mb_r05::line_finish<Alg, OUT_ALIGNED>(st, w0, w1, tm, tp, t, nfull, K, rec_len, out, g * 64 + lane, n_rec);
         v0 = (v0 + K + 1 + NS - 1) / NS * NS;
         g += G * C;
         if (g >= n_groups)

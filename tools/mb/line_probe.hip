@@ -40,6 +40,7 @@ __device__ inline uint64_t pr_rt()
 
 #include "digest_dma.h"
 #include "line1_kernel.h"
+#include "line_r05_kernel.h"
 #include "md5_device.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
@@ -81,7 +82,7 @@ static void launch(const void *k, unsigned grid, unsigned bs, const uint8_t *src
         return;
     }
     const uint64_t groups = (n + 63) / 64, rounds = (groups + grid - 1) / grid;
-    uint32_t *slot = g_pool_ring + (g_pool_next++ % brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords;
+    uint32_t *slot = g_pool_ring + (g_pool_next++ % brb_mb_r05::kPoolSlots) * brb_mb_r05::kPoolSlotWords;
     uint32_t t_own = uint32_t(rounds - uint64_t(pool_rounds));
     void *args[] = {&src, &L, &n, &o, &slot, &t_own};
     if (hipLaunchKernel(k, dim3(grid), dim3(bs), args, 0, 0) != hipSuccess) { printf("launch failed\n"); exit(1); }
@@ -111,8 +112,8 @@ int main(int argc, char **argv)
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_probe), &pr, sizeof(pr)));
     struct V { const char *name; Kern k; };
     struct VG { const char *name; const void *k; int waves; int pool = -1; };
-    CK(hipMalloc(&g_pool_ring, size_t(brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords * 4));
-    CK(hipMemset(g_pool_ring, 0, size_t(brb_digest::kPoolSlots) * brb_digest::kPoolSlotWords * 4));
+    CK(hipMalloc(&g_pool_ring, size_t(brb_mb_r05::kPoolSlots) * brb_mb_r05::kPoolSlotWords * 4));
+    CK(hipMemset(g_pool_ring, 0, size_t(brb_mb_r05::kPoolSlots) * brb_mb_r05::kPoolSlotWords * 4));
     VG vs64[] = {{"DMA64 static 4x4", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 4, 2, 1, true>, 4},
                  {"DMA64 dyn16", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 16, 2, 1, true, false, true>, 16},
                  {"DMA64 dyn8", (const void *)(Kern)brb_digest::digest_fixed_dma_kernel<AlgLit, 8, 2, 1, true, false, true>, 8},
@@ -121,29 +122,29 @@ int main(int argc, char **argv)
     // argv[3] = "pool": the product line kernel without and with the tail pool (4 / 8 / 16 rounds),
     // the static split with SIMD partners in lockstep (LOCK) and without, interleaved twice (VERDICT
     // r04 item 2: the workgroup-end spread)
-    VG vp[] = {{"LINE nopool", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
-               {"LINE lock", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
-               {"LINE static", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false>, 8, 0},
-               {"LINE pool8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
-               {"LINE pool4", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
-               {"LINE pool16", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16},
-               {"LINE nopool #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
-               {"LINE lock #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
-               {"LINE pool8 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
-               {"LINE pool4 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
-               {"LINE pool16 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16}};
-    VG vs[] = {{"LINE md5 nt dyn8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+    VG vp[] = {{"LINE nopool", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE lock", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
+               {"LINE static", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, false>, 8, 0},
+               {"LINE pool8", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
+               {"LINE pool4", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
+               {"LINE pool16", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16},
+               {"LINE nopool #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+               {"LINE lock #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, false, false, true>, 8, 0},
+               {"LINE pool8 #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 8},
+               {"LINE pool4 #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 4},
+               {"LINE pool16 #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true, true>, 8, 16}};
+    VG vs[] = {{"LINE md5 nt dyn8", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
               {"LINE1 ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
               {"LINE1 ns2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
               {"LINE1 ns2 u4", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
               {"LINE1 ns3 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3, true>, -4},
               {"LINE1 ns2 spread", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, true>, -4},
-              {"LINE md5 nt dyn8 #2", (const void *)(KernL)brb_digest::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
+              {"LINE md5 nt dyn8 #2", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, 8, 0},
               {"LINE1 ns3 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 3>, -4},
               {"LINE1 ns2 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2>, -4},
               {"LINE1 ns2 u4 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
               {"LINE1 dma-only ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
-              {"LINE dma-only nt dyn8", (const void *)(KernL)brb_digest::digest_line_kernel<AlgNull, 8, true, true, true>, 8, 0}};
+              {"LINE dma-only nt dyn8", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgNull, 8, true, true, true>, 8, 0}};
     int it = 0;
     const bool small = L <= 64;
     const bool pool = argc > 3 && std::string(argv[3]) == "pool";

@@ -10,6 +10,7 @@
 
 #include "digest_dma.h"
 #include "digest_line.h"
+#include "line_r05_kernel.h"   // the round-1..5 line kernel forms (static / ticketed, nt or not)
 #include "md5_device.h"
 #include "md5_sched.h"
 
@@ -139,13 +140,13 @@ int main(int argc, char **argv)
     if (L > 64) vs = {
         {"BPS2 P2 xad (product)", digest_fixed_dma_kernel<AlgLit, 4, 2, 2, true>, 4, 512},
         {"BPS2 P2 dyn8 1WG/CU", digest_fixed_dma_kernel<AlgLit, 8, 2, 2, true, false, true>, 8, -256},
-        {"LINE (line-aligned) P2", digest_line_kernel<AlgLit, 4, true>, 4, 512},
-        {"LINE nt", digest_line_kernel<AlgLit, 4, true, true>, 4, 512},
-        {"LINE nt dyn8 1WG/CU", digest_line_kernel<AlgLit, 8, true, true, true>, 8, -256},
-        {"LINE nt dyn4 2WG/CU", digest_line_kernel<AlgLit, 4, true, true, true>, 4, -512},
-        {"LINE dyn8 1WG/CU", digest_line_kernel<AlgLit, 8, true, false, true>, 8, -256},
-        {"DMA only LINE", digest_line_kernel<AlgNull, 4, true>, 4, 512},
-        {"DMA only LINE nt", digest_line_kernel<AlgNull, 4, true, true>, 4, 512},
+        {"LINE (line-aligned) P2", (Kern)brb_mb_r05::digest_line_kernel<AlgLit, 4, true>, 4, 512},
+        {"LINE nt", (Kern)brb_mb_r05::digest_line_kernel<AlgLit, 4, true, true>, 4, 512},
+        {"LINE nt dyn8 1WG/CU", (Kern)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, 8, -256},
+        {"LINE nt dyn4 2WG/CU", (Kern)brb_mb_r05::digest_line_kernel<AlgLit, 4, true, true, true>, 4, -512},
+        {"LINE dyn8 1WG/CU", (Kern)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, false, true>, 8, -256},
+        {"DMA only LINE", (Kern)brb_mb_r05::digest_line_kernel<AlgNull, 4, true>, 4, 512},
+        {"DMA only LINE nt", (Kern)brb_mb_r05::digest_line_kernel<AlgNull, 4, true, true>, 4, 512},
         {"DMA only BPS2 P2", digest_fixed_dma_kernel<AlgNull, 4, 2, 2, true>, 4, 512},
         {"DMA only BPS2 P2 nt", digest_fixed_dma_kernel<AlgNull, 4, 2, 2, true, true>, 4, 512},
         {"read floor 1024x256", read_floor<false>, 4, -1024},
