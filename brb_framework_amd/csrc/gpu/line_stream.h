@@ -250,6 +250,11 @@ BRB_DEV void plan_whole(const brb_md5::FunnelT<RW> &f, uint32_t b, Emit &p)
     p.tail = 0;
 }
 
+// Round 6: when no writing lane's half wraps around its ring, the words go
+// out without the wrap mask -- a whole half as one base address and the ds_write instruction
+// offsets (1 VALU per word: the funnel shift), a boundary half with the clamp on unmasked ring
+// addresses (3 instead of 4).  Whether any lane wraps is one ballot per half (wave-uniform branch);
+// with RW = 64 a whole half wraps in at most one of four consecutive halves.
 template <uint32_t RW, int H, bool WHOLE>
 BRB_DEV void emit_half(brb_md5::FunnelT<RW> &f, Emit &p, const uint32_t (&dw)[36])
 {
@@ -260,6 +265,37 @@ BRB_DEV void emit_half(brb_md5::FunnelT<RW> &f, Emit &p, const uint32_t (&dw)[36
     const int top = p.iw < hi ? p.iw : hi;
     const uint32_t n = WHOLE ? uint32_t(H ? 32 : 16) : uint32_t(top > p.i0 ? top - p.i0 : 0);
     const uint32_t ahi = p.alo + (n << 8);
+    const uint32_t s0 = p.wpos0 & (RW - 1);                   // ring slot of word i0 (whole: word 0)
+    if (WHOLE) {
+        // this half's 16 words go to slots s0 + 16 H .. + 15
+        const uint32_t s = (s0 + 16u * H) & (RW - 1);
+        if (__builtin_amdgcn_ballot_w64(s > RW - 16) == 0) {
+            const uint32_t base = f.ring | (f.lane4 + (s << 8));
+#pragma unroll
+            for (int i = lo < 0 ? 0 : lo; i < hi; i++)
+                brb_md5::FunnelT<RW>::lds_st(base + uint32_t((i - (lo < 0 ? 0 : lo)) << 8),
+                                             __builtin_amdgcn_alignbit(dw[i + 1], dw[i], p.sh));
+            f.wpos = p.wpos0 + n;
+            return;
+        }
+    } else if (__builtin_amdgcn_ballot_w64(s0 + n > RW - 1) == 0) {
+        // slots s0 .. s0 + n (the last one the clamp's free slot) lie inside the ring: clamp on
+        // unmasked addresses (signed: a word before i0 may compute below the ring's base)
+        const int alo = int(f.ring | (f.lane4 + (s0 << 8)));
+        const int ahi2 = alo + int(n << 8);
+        const int abase = alo - (p.i0 << 8);
+#pragma unroll
+        for (int i = lo; i < hi; i++) {
+            const uint32_t v = __builtin_amdgcn_alignbit(dw[i + 1], dw[i < 0 ? 0 : i], p.sh);
+            int a = abase + (i << 8);
+            asm("v_med3_i32 %0, %1, %2, %3" : "=v"(a) : "v"(a), "v"(alo), "v"(ahi2));   // before i0 -> wpos0, past the range -> free slot
+            brb_md5::FunnelT<RW>::lds_st(uint32_t(a), v);
+        }
+        if (p.hmask && p.i0 >= lo && p.i0 < hi && p.i0 < p.iw)   // the head, over word i0's slot
+            brb_md5::FunnelT<RW>::lds_st(uint32_t(alo), p.head);
+        f.wpos = p.wpos0 + n;
+        return;
+    }
 #pragma unroll
     for (int i = lo; i < hi; i++) {
         if (WHOLE && i < 0)

@@ -48,9 +48,13 @@ struct Perm {
 //   * S[i] is read two bytes ahead (positions i+1, i+2 in flight), before the swap of its step is
 //     written; a raw S[i_{T+1}] missed swaps T-2, T-1 and T, and since i_s != i_{T+1} for those,
 //     only j_s == i_{T+1} -> a_s applies (three compare/select pairs).
-// So j_{T+1} = j_T + a_{T+1} is pure VALU.  Indices are kept as running 32-bit sums (2^32 is a
-// multiple of 256); an LDS address is one v_perm_b32 of the sum's low byte and the lane's column,
-// and the patches compare addresses, so no masking op is needed anywhere.
+// So j_{T+1} = j_T + a_{T+1} is pure VALU.  Indices live only as their LDS addresses, 16-bit values
+// index << 8 | column (round 6): the next i is one v_pk_add_u16 of 256 and the
+// next j one v_pk_mad_u16 (a_{T+1} * 256 + address of j_T).  The low halves wrap mod 2^16, i.e. the
+// index mod 256, and the high halves add zeros, so the result stays a clean 16-bit address
+// (tools/mb/u16_check.hip; the plain v_add_u16 / v_mad_u16 leave the destination's high half as it
+// was on gfx950).  Round 5 kept running 32-bit sums and paid an add and a v_perm_b32 for each.  The patches compare addresses, so no masking op is needed
+// anywhere.
 // Before the first byte the "previous swaps" are identity swaps (S[ci] = S[ci], S[cj] = S[cj]),
 // which patch nothing wrongly, so there is no special case.  One byte is always started ahead of
 // the last one returned; store() drops it (its swap was never written), so the state advances by
@@ -60,21 +64,38 @@ struct Perm {
 // two steps of read-ahead ran 178 and 195 us.  Round 2 (session 4), interleaved A/B (rocprofv3): reading
 // S[j] after the swap instead of patching it took the RC4 pass 123.0 -> 117.4 us, the frame kernel
 // 141.2 -> 130.0 us and the open kernel 138.1 -> 124.7 us; moving the S[i] read after the swap too
-// (one pair fewer) ran 128 us: the read then lands too late for the step that needs it.
+// (one pair fewer) ran 128 us: the read then lands too late for the step that needs it.  Round 6,
+// with the 16-bit address ops (11.3 VALU per byte): reading S[j_{T+1}] before swap T again (patched
+// with swap T-1 at completion, 15.3 VALU per byte) ran 102.5 -> 125.9 us (interleaved, three
+// rounds, profiles/r06/ab_rc4.txt); the exact read after the swap stays.
 struct Gen {
     Perm P;
-    // Every index is kept as (running 32-bit sum, LDS address).  Two indices are equal mod 256 iff
-    // their addresses are (same lane column), so all compares are on addresses.
-    // started byte T: j (sum), S[i_T], raw S[j_T], addresses of S[i_T] and S[j_T]
-    uint32_t j, a, rb, ai, aj;
+    // Every index is kept as its LDS address.  Two indices are equal mod 256 iff their addresses
+    // are (same lane column), so all compares are on addresses.
+    // started byte T: S[i_T], raw S[j_T], addresses of S[i_T] and S[j_T]
+    uint32_t a, rb, ai, aj;
     // swap T-1 (written): addresses of i and j, a; swap T-2: address of j, a
     uint32_t pai, paj, pa, qaj, qa;
-    // S[i] read ahead: positions i_T + 1 and i_T + 2 (running sums), raw values, addresses
-    uint32_t p1, r1, ad1, p2, r2, ad2;
+    // S[i] read ahead: positions i_T + 1 and i_T + 2: raw values, addresses
+    uint32_t r1, ad1, r2, ad2;
     uint32_t tail;     // dword 64 of the state: index1, index2 and the two bytes after them
 
     // LDS address of index x (low byte of x): byte 1 = x, byte 0 = the lane's column
     BRB_DEV uint32_t ad(uint32_t x) const { return __builtin_amdgcn_perm(x, P.lw, 0x0C0C0400u); }
+    // address of the index after the one at address x: (x + 256) mod 2^16 (x < 2^16)
+    static BRB_DEV uint32_t ad_next(uint32_t x)
+    {
+        uint32_t r;
+        asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(256u));
+        return r;
+    }
+    // address of (the index at address x) + v: (v * 256 + x) mod 2^16 (x < 2^16, v < 2^16)
+    static BRB_DEV uint32_t ad_plus(uint32_t x, uint32_t v)
+    {
+        uint32_t r;
+        asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(v), "s"(256u), "v"(x));
+        return r;
+    }
     BRB_DEV uint32_t rd(uint32_t a_) const { return P.lds[a_]; }
     BRB_DEV void wr(uint32_t a_, uint32_t v) const { P.lds[a_] = uint8_t(v); }
 
@@ -98,14 +119,11 @@ struct Gen {
         qa = pa;
         ai = ad(ci + 1);
         a = rd(ai);
-        j = cj + a;
-        aj = ad(j);
+        aj = ad(cj + a);
         rb = rd(aj);
-        p1 = ci + 2;
-        ad1 = ad(p1);
+        ad1 = ad(ci + 2);
         r1 = rd(ad1);
-        p2 = ci + 3;
-        ad2 = ad(p2);
+        ad2 = ad(ci + 3);
         r2 = rd(ad2);
     }
 
@@ -122,15 +140,13 @@ struct Gen {
     // Completes byte T (returns its keystream byte) and starts byte T+1.
     BRB_DEV uint32_t step()
     {
-        // ---- start byte T+1 at position p1
+        // ---- start byte T+1 at address ad1
         uint32_t a1 = r1;                    // read before swap T-2 was written
         a1 = qaj == ad1 ? qa : a1;           // swap T-2
         a1 = paj == ad1 ? pa : a1;           // swap T-1
         a1 = aj == ad1 ? a : a1;             // swap T (not written yet)
-        const uint32_t j1 = j + a1;
-        const uint32_t aj1 = ad(j1);
-        const uint32_t p3 = p2 + 1;
-        const uint32_t ad3 = ad(p3);
+        const uint32_t aj1 = ad_plus(aj, a1);   // j_{T+1} = j_T + a_{T+1}
+        const uint32_t ad3 = ad_next(ad2);
         const uint32_t r3 = rd(ad3);         // S[i_{T+1} + 2], sees swaps <= T-1
         // ---- complete byte T
         const uint32_t b = rb;               // S[j_T], read after swap T-1 was written: exact
@@ -144,15 +160,12 @@ struct Gen {
         pai = ai;
         paj = aj;
         pa = a;
-        j = j1;
         a = a1;
         rb = rb1;
         ai = ad1;
         aj = aj1;
-        p1 = p2;
         r1 = r2;
         ad1 = ad2;
-        p2 = p3;
         r2 = r3;
         ad2 = ad3;
         return k;
