@@ -236,6 +236,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_
 
     BRB_LINE_PROBE_DECL
     BRB_LINE_PROBE(0);
+    // (Round 6: issuing this first line pair before the workgroup barrier that publishes the ticket
+    // counter measured 297-301 us against 295-297 us on the cfg5 shard, cfg2 unchanged: not kept,
+    // profiles/r06/early_dma_ab.txt.)
     desc(g, rs);
     issue(rs, so, P, true);
     issue(rs, so, P ^ 1, true);
