@@ -133,7 +133,9 @@ def main():
                                ("pmc_seg", "f4_md5seg", "md5_seg_", 1),
                                ("pmc_b64", "f4_base64", "b64_", 2),
                                ("pmc_md5var", "var_md5var", "Md5Alg", 1),
-                               ("pmc_sha1var", "var_sha1var", "Sha1Alg", 1)):
+                               ("pmc_sha1var", "var_sha1var", "Sha1Alg", 1),
+                               # the cfg5 shard shape (1 Mi x 1500 B per GPU) as the timed batch
+                               ("pmc5", "cfg5_md5", "Md5Alg", 1)):
         d = os.path.join(src, sub)
         if not os.path.isdir(d):
             continue

@@ -11,8 +11,9 @@ declare -A ARGS=(
   [pmc4]="--config 4"        [pmc_rc4]="--op rc4"            [pmc_rc4md5]="--op rc4md5"
   [pmc_md]="--op metadata"   [pmc_seg]="--op md5seg"         [pmc_b64]="--op base64"
   [pmc_md5var]="--op md5var" [pmc_sha1var]="--op sha1var"
+  [pmc5]="--records-per-gpu 1048576"
 )
-PASSES=${@:-pmc2 pmc2s pmc3 pmc4 pmc_rc4 pmc_rc4md5 pmc_md pmc_seg pmc_b64 pmc_md5var pmc_sha1var}
+PASSES=${@:-pmc2 pmc2s pmc3 pmc4 pmc_rc4 pmc_rc4md5 pmc_md pmc_seg pmc_b64 pmc_md5var pmc_sha1var pmc5}
 for d in $PASSES; do
   bash tools/gpu_pmc.sh "$T/$d" ${ARGS[$d]} > /dev/null || { echo "$d failed"; exit 1; }
   echo "$d ok"
