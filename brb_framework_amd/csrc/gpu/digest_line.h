@@ -100,7 +100,9 @@ inline bool line_tail_hi(uint32_t rec_len)
 // (1 Mi x 1500 B, tools/mb/line_probe.hip); with tickets the faster wave simply takes more groups.
 // One 8-wave workgroup per CU (128 KiB of LDS), two waves per SIMD.  Two ways of evening out the
 // end of a launch measured slower and live in tools/mb/line_r05_kernel.h: a chip-wide tail pool
-// and SIMD partners in lockstep.
+// and SIMD partners in lockstep.  Round 6: one ticket counter per SIMD (SIMD s of
+// a workgroup owning its rounds s, s + 4, ...) measured the same on the cfg5 shard (289.95 vs
+// 290.45 us) and 1 % slower at 300 001 records (profiles/r06/line_ab_*_box4_simd_tickets.txt).
 template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data,
                                                                              uint32_t rec_len, uint64_t n_rec,
