@@ -103,6 +103,9 @@ inline bool line_tail_hi(uint32_t rec_len)
 // and SIMD partners in lockstep.  Round 6: one ticket counter per SIMD (SIMD s of
 // a workgroup owning its rounds s, s + 4, ...) measured the same on the cfg5 shard (289.95 vs
 // 290.45 us) and 1 % slower at 300 001 records (profiles/r06/line_ab_*_box4_simd_tickets.txt).
+// Loading one dword of each row's line k+2 right after line k+1's DMA (temporal policy, into an LDS
+// scratch row) so that its DMA would hit the L2 one iteration later: cfg5 297.0 -> 322.0 us, cfg2
+// 21.3 -> 24.1 us (profiles/r06/line_ab_*_box5_l2prefetch.txt): not kept.
 template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_kernel(const uint8_t *__restrict__ data,
                                                                              uint32_t rec_len, uint64_t n_rec,
