@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "digest_line.h"
+#include "line4_kernel.h"
 #include "line_r05_kernel.h"
 #include "md5_device.h"
 
@@ -37,6 +38,7 @@ struct Var {
     const char *name;
     const void *k;
     bool six;     // round-5 signature (pool heads, t_own)
+    unsigned threads = 512;
 };
 
 static void launch(const Var &v, unsigned grid, const uint8_t *src, uint32_t L, uint64_t n, uint8_t *o)
@@ -45,7 +47,7 @@ static void launch(const Var &v, unsigned grid, const uint8_t *src, uint32_t L, 
     uint32_t t_own = 0;
     void *a4[] = {&src, &L, &n, &o};
     void *a6[] = {&src, &L, &n, &o, &pool, &t_own};
-    CK(hipLaunchKernel(v.k, dim3(grid), dim3(512), v.six ? a6 : a4, 0, 0));
+    CK(hipLaunchKernel(v.k, dim3(grid), dim3(v.threads), v.six ? a6 : a4, 0, 0));
 }
 
 static double med(std::vector<double> v)
@@ -79,6 +81,9 @@ int main(int argc, char **argv)
         {"r05 per-group setup", (const void *)(K6)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, true},
         {"r06 hoisted", hi ? (const void *)(K4)brb_digest::digest_line_kernel<AlgLit, 8, true, true>
                            : (const void *)(K4)brb_digest::digest_line_kernel<AlgLit, 8, true, false>, false},
+        {"half-line 16 waves", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 16, true>, false, 1024},
+        {"half-line 8 waves", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 8, true>, false, 512},
+        {"half-line 16 w, all L2", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 16, true, true>, false, 1024},
     };
     const int nv = int(sizeof(vs) / sizeof(vs[0]));
     // parity between the variants, on every copy's first launch
