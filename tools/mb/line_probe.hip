@@ -39,6 +39,7 @@ __device__ inline uint64_t pr_rt()
     } while (0)
 
 #include "digest_dma.h"
+#include "digest_line.h"
 #include "line1_kernel.h"
 #include "line_r05_kernel.h"
 #include "md5_device.h"
@@ -145,12 +146,21 @@ int main(int argc, char **argv)
               {"LINE1 ns2 u4 #2", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgLit, true, true, 2, false, 4>, -4},
               {"LINE1 dma-only ns3", (const void *)(Kern)brb_digest::digest_line1_kernel<AlgNull, true, true, 3>, -4},
               {"LINE dma-only nt dyn8", (const void *)(KernL)brb_mb_r05::digest_line_kernel<AlgNull, 8, true, true, true>, 8, 0}};
+    // argv[3] = "r06": the product kernel (digest_line.h, round 6) twice and its DMA-only form
+    const bool hi = brb_digest::line_tail_hi(L);
+    VG v6[] = {{"r06 product", hi ? (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true>
+                                  : (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, false>, 8},
+               {"r06 dma-only", hi ? (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, true>
+                                   : (const void *)(Kern)brb_digest::digest_line_kernel<AlgNull, 8, true, false>, 8},
+               {"r06 product #2", hi ? (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, true>
+                                     : (const void *)(Kern)brb_digest::digest_line_kernel<AlgLit, 8, true, false>, 8}};
     int it = 0;
     const bool small = L <= 64;
     const bool pool = argc > 3 && std::string(argv[3]) == "pool";
-    const int nv = small ? 4 : pool ? int(sizeof(vp) / sizeof(vp[0])) : int(sizeof(vs) / sizeof(vs[0]));
+    const bool r06 = argc > 3 && std::string(argv[3]) == "r06";
+    const int nv = small ? 4 : pool ? int(sizeof(vp) / sizeof(vp[0])) : r06 ? 3 : int(sizeof(vs) / sizeof(vs[0]));
     for (int vi = 0; vi < nv; vi++) {
-        const VG &v = small ? vs64[vi] : pool ? vp[vi] : vs[vi];
+        const VG &v = small ? vs64[vi] : pool ? vp[vi] : r06 ? v6[vi] : vs[vi];
         // 4-wave workgroups: 2 per CU (4 for <= 64 B records); bigger (dyn): one per CU
         const unsigned grid = v.waves == -4 ? unsigned((groups + 3) / 4)
                               : v.waves == 4 ? unsigned(std::min<uint64_t>((groups + 3) / 4, small ? 1024 : 512))
