@@ -24,7 +24,7 @@ __device__ inline uint64_t pr_rt()
     return t;
 }
 #define BRB_LINE_PROBE 1
-#define NP 6
+#define NP 8
 #define BRB_LINE_PROBE_DECL uint64_t pr_c0 = 0, pr_r0 = 0, pr_tw = 0, pr_wait = 0, pr_first = 0;
 #define BRB_LINE_PROBE(ev)                                                              \
     do {                                                                                \
@@ -35,6 +35,10 @@ __device__ inline uint64_t pr_rt()
             uint64_t *o = g_probe + NP * wave0;                                         \
             o[0] = pr_c0; o[1] = pr_clk(); o[2] = pr_r0; o[3] = pr_rt(); o[4] = pr_wait;\
             o[5] = pr_first;                                                            \
+            uint32_t xcc_, hw_;                                                         \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_));   \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));           \
+            o[6] = xcc_; o[7] = hw_;                                                    \
         }                                                                               \
     } while (0)
 
@@ -207,6 +211,18 @@ int main(int argc, char **argv)
             dur.push_back(rt / 1000.0);
             wf.push_back(double(q[4]) / double(q[1] - q[0]));
             fw.push_back(double(q[5]) / (double(q[1] - q[0]) / dur.back()));   // us
+        }
+        {   // per-XCD (HW_REG_XCC_ID) median in-kernel clock, mean end, wave count
+            printf("  per-XCC (hw): ");
+            for (int x = 0; x < 8; x++) {
+                std::vector<double> cm, ce;
+                for (uint64_t w = 0; w < nw; w++)
+                    if (hp[NP * w + 6] == uint64_t(x)) { cm.push_back(mhz[w]); ce.push_back(en[w]); }
+                if (cm.empty()) continue;
+                double se = 0; for (double e : ce) se += e;
+                printf(" x%d: %zu waves %.0f MHz end %.1f |", x, cm.size(), pct(cm, .5), se / ce.size());
+            }
+            printf("\n");
         }
         {   // per-XCD (blockIdx % 8) mean end time, and a histogram of end times
             double sx[8] = {0}; int cx[8] = {0};
