@@ -234,3 +234,73 @@ def test_batcher_all_devices(brb, orc, torch_dev, parts, zero_copy, pipelined):
             assert got[c] == want[c], c
             assert b.state(c, 0) == ours_r[c] and b.state(c, 1) == ours_w[c]
         b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["async", "sync"])
+def test_batcher_all_devices_fault_poisons(brb, orc, torch_dev, how):
+    """The round-6 poisoning contract (test_batcher.py::test_pipelined_fault_poisons_next_round)
+    through BRB_BATCHER_ALL_DEVICES with the connections over 3 sub-batchers: round A faults (test
+    option pair_stall) on every sub, round B was submitted behind it, and every sub poisons its own
+    connections of A.  Compared per connection (subs deliver one after another)."""
+    with brb.TestOption("devices", 3):
+        rng = np.random.default_rng(77 if how == "async" else 78)
+        C, CA = 96, 80
+        keys = [rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(C)]
+        b = brb.TransformBatcher(C, 4 << 20, 2, pipelined=True, all_devices=True)
+        st = {}
+
+        def rekey(conns):
+            for c in conns:
+                b.enable(c, keys[c])
+                st[c] = [orc.rc4_init(keys[c]) for _ in range(3)]
+
+        def submit(c, rnd):
+            n = int(rng.choice([0, 17, 700, 1500]))
+            payload = workload.gen_records(0x5EED00F9 + rnd, c, 1, n).tobytes() if n else b""
+            r, w, pw = st[c]
+            pw, frame = orc.rc4md5_frame(pw, payload, c)
+            r, dec, ok = orc.rc4md5_open(r, frame)
+            assert b.read(c, frame) == 1
+            w, out = orc.rc4md5_frame(w, payload, rnd + c)
+            assert b.write(c, payload, rnd + c) == 1
+            st[c] = [r, w, pw]
+            return [(0, dec, ok), (1, out, 1)]
+
+        drop = [(0, b"", brb.TRANSFORM_DROPPED), (1, b"", brb.TRANSFORM_DROPPED)]
+        want = {c: [] for c in range(C)}
+        got = {c: [] for c in range(C)}
+
+        def take(results):
+            for conn, op, out, valid in results:
+                got[conn].append((op, out, valid))
+
+        rekey(range(C))
+        for c in range(CA):
+            submit(c, 0)
+            want[c] += drop
+        with brb.TestOption("rc4md5_pair", 1), brb.TestOption("pair_stall", 1):
+            assert b.flush_async() == []
+        for c in range(C):
+            e = submit(c, 1)
+            want[c] += drop if c < CA else e
+        with pytest.raises(RuntimeError, match="dropped") as ei:
+            b.flush_async() if how == "async" else b.flush()
+        assert ei.value.code == brb.BATCH_DROPPED
+        take(ei.value.results)
+        assert b.read(0, b"refused") == -1 and b.write(CA - 1, b"refused", 0) == -1
+        try:
+            take(b.flush())
+        except RuntimeError as e:                 # async: B's poisoned buffers come back here
+            assert e.code == brb.BATCH_DROPPED
+            take(e.results)
+        for c in range(C):
+            assert got[c] == want[c], c
+        rekey(range(CA))
+        for c in range(C):
+            want[c] += submit(c, 3)
+        take(b.flush())
+        for c in range(C):
+            assert got[c] == want[c], c
+            assert b.state(c, 0) == st[c][0] and b.state(c, 1) == st[c][1]
+        b.close()
