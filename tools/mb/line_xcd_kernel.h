@@ -25,7 +25,8 @@ BRB_DEV inline uint64_t rt_now()
     return t;
 }
 
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI>
+// POL (streamed lines 2..K of a group): 0 nt (the product's), 1 nt sc1, 2 sc1, 3 sc0 sc1, 4 nt sc0 sc1
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI, int POL = 0>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const uint8_t *__restrict__ data,
                                                                        uint32_t rec_len, uint64_t n_rec,
                                                                        uint8_t *__restrict__ out, XSplit xs,
@@ -119,10 +120,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const ui
                  : "v"(vq[0]), "v"(vq[1]), "v"(vq[2]), "v"(vq[3]), "v"(vq[4]), "v"(vq[5]), "v"(vq[6]), \
                    "v"(vq[7]), "s"(rs), "s"(m), "s"(m + 4096u), "s"(so)                           \
                  : "memory")
-        if (!keep_l2)
-            BRB_XCD_DMA8("nt ");
-        else
+        if (keep_l2)
             BRB_XCD_DMA8("");
+        else if (POL == 1)
+            BRB_XCD_DMA8("nt sc1 ");
+        else if (POL == 2)
+            BRB_XCD_DMA8("sc1 ");
+        else if (POL == 3)
+            BRB_XCD_DMA8("sc0 sc1 ");
+        else if (POL == 4)
+            BRB_XCD_DMA8("nt sc0 sc1 ");
+        else
+            BRB_XCD_DMA8("nt ");
 #undef BRB_XCD_DMA8
         so += 128;
     };
