@@ -11,12 +11,92 @@
 #pragma once
 
 #include "digest_line.h"
+#include "md5_device.h"
 
 namespace brb_mb_xcd {
 
 struct XSplit {
     uint32_t s[9];    // prefix sums of groups per class; s[8] = n_groups
 };
+
+// MD5 compression with a hook after step 15 (round 1 has consumed m[0..15] in order): the
+// STAGE 2 form of the kernel below issues its refill DMA there.
+template <class Hook>
+BRB_DEV void md5_compress_hk(Md5State &st, const uint32_t (&m)[16], Hook hook)
+{
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    BRB_MD5_STEP(BRB_MD5_F1, a, b, c, d, m[0], 0xd76aa478u, 7);
+    BRB_MD5_STEP(BRB_MD5_F1, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    BRB_MD5_STEP(BRB_MD5_F1, c, d, a, b, m[2], 0x242070dbu, 17);
+    BRB_MD5_STEP(BRB_MD5_F1, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    BRB_MD5_STEP(BRB_MD5_F1, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    BRB_MD5_STEP(BRB_MD5_F1, d, a, b, c, m[5], 0x4787c62au, 12);
+    BRB_MD5_STEP(BRB_MD5_F1, c, d, a, b, m[6], 0xa8304613u, 17);
+    BRB_MD5_STEP(BRB_MD5_F1, b, c, d, a, m[7], 0xfd469501u, 22);
+    BRB_MD5_STEP(BRB_MD5_F1, a, b, c, d, m[8], 0x698098d8u, 7);
+    BRB_MD5_STEP(BRB_MD5_F1, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    BRB_MD5_STEP(BRB_MD5_F1, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    BRB_MD5_STEP(BRB_MD5_F1, b, c, d, a, m[11], 0x895cd7beu, 22);
+    BRB_MD5_STEP(BRB_MD5_F1, a, b, c, d, m[12], 0x6b901122u, 7);
+    BRB_MD5_STEP(BRB_MD5_F1, d, a, b, c, m[13], 0xfd987193u, 12);
+    BRB_MD5_STEP(BRB_MD5_F1, c, d, a, b, m[14], 0xa679438eu, 17);
+    BRB_MD5_STEP(BRB_MD5_F1, b, c, d, a, m[15], 0x49b40821u, 22);
+    __builtin_amdgcn_sched_barrier(0);
+    hook();
+    __builtin_amdgcn_sched_barrier(0);
+    BRB_MD5_STEP(BRB_MD5_F2, a, b, c, d, m[1], 0xf61e2562u, 5);
+    BRB_MD5_STEP(BRB_MD5_F2, d, a, b, c, m[6], 0xc040b340u, 9);
+    BRB_MD5_STEP(BRB_MD5_F2, c, d, a, b, m[11], 0x265e5a51u, 14);
+    BRB_MD5_STEP(BRB_MD5_F2, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    BRB_MD5_STEP(BRB_MD5_F2, a, b, c, d, m[5], 0xd62f105du, 5);
+    BRB_MD5_STEP(BRB_MD5_F2, d, a, b, c, m[10], 0x02441453u, 9);
+    BRB_MD5_STEP(BRB_MD5_F2, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    BRB_MD5_STEP(BRB_MD5_F2, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    BRB_MD5_STEP(BRB_MD5_F2, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    BRB_MD5_STEP(BRB_MD5_F2, d, a, b, c, m[14], 0xc33707d6u, 9);
+    BRB_MD5_STEP(BRB_MD5_F2, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    BRB_MD5_STEP(BRB_MD5_F2, b, c, d, a, m[8], 0x455a14edu, 20);
+    BRB_MD5_STEP(BRB_MD5_F2, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    BRB_MD5_STEP(BRB_MD5_F2, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    BRB_MD5_STEP(BRB_MD5_F2, c, d, a, b, m[7], 0x676f02d9u, 14);
+    BRB_MD5_STEP(BRB_MD5_F2, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    BRB_MD5_STEP3X(a, b, c, d, m[5], 0xfffa3942u, 4);
+    BRB_MD5_STEP3X(d, a, b, c, m[8], 0x8771f681u, 11);
+    BRB_MD5_STEP3X(c, d, a, b, m[11], 0x6d9d6122u, 16);
+    BRB_MD5_STEP3X(b, c, d, a, m[14], 0xfde5380cu, 23);
+    BRB_MD5_STEP3X(a, b, c, d, m[1], 0xa4beea44u, 4);
+    BRB_MD5_STEP3X(d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    BRB_MD5_STEP3X(c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    BRB_MD5_STEP3X(b, c, d, a, m[10], 0xbebfbc70u, 23);
+    BRB_MD5_STEP3X(a, b, c, d, m[13], 0x289b7ec6u, 4);
+    BRB_MD5_STEP3X(d, a, b, c, m[0], 0xeaa127fau, 11);
+    BRB_MD5_STEP3X(c, d, a, b, m[3], 0xd4ef3085u, 16);
+    BRB_MD5_STEP3X(b, c, d, a, m[6], 0x04881d05u, 23);
+    BRB_MD5_STEP3X(a, b, c, d, m[9], 0xd9d4d039u, 4);
+    BRB_MD5_STEP3X(d, a, b, c, m[12], 0xe6db99e5u, 11);
+    BRB_MD5_STEP3X(c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    BRB_MD5_STEP3X(b, c, d, a, m[2], 0xc4ac5665u, 23);
+    BRB_MD5_STEP(BRB_MD5_F4, a, b, c, d, m[0], 0xf4292244u, 6);
+    BRB_MD5_STEP(BRB_MD5_F4, d, a, b, c, m[7], 0x432aff97u, 10);
+    BRB_MD5_STEP(BRB_MD5_F4, c, d, a, b, m[14], 0xab9423a7u, 15);
+    BRB_MD5_STEP(BRB_MD5_F4, b, c, d, a, m[5], 0xfc93a039u, 21);
+    BRB_MD5_STEP(BRB_MD5_F4, a, b, c, d, m[12], 0x655b59c3u, 6);
+    BRB_MD5_STEP(BRB_MD5_F4, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    BRB_MD5_STEP(BRB_MD5_F4, c, d, a, b, m[10], 0xffeff47du, 15);
+    BRB_MD5_STEP(BRB_MD5_F4, b, c, d, a, m[1], 0x85845dd1u, 21);
+    BRB_MD5_STEP(BRB_MD5_F4, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    BRB_MD5_STEP(BRB_MD5_F4, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    BRB_MD5_STEP(BRB_MD5_F4, c, d, a, b, m[6], 0xa3014314u, 15);
+    BRB_MD5_STEP(BRB_MD5_F4, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    BRB_MD5_STEP(BRB_MD5_F4, a, b, c, d, m[4], 0xf7537e82u, 6);
+    BRB_MD5_STEP(BRB_MD5_F4, d, a, b, c, m[11], 0xbd3af235u, 10);
+    BRB_MD5_STEP(BRB_MD5_F4, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    BRB_MD5_STEP(BRB_MD5_F4, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+}
 
 BRB_DEV inline uint64_t rt_now()
 {
@@ -26,7 +106,11 @@ BRB_DEV inline uint64_t rt_now()
 }
 
 // POL (streamed lines 2..K of a group): 0 nt (the product's), 1 nt sc1, 2 sc1, 3 sc0 sc1, 4 nt sc0 sc1
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI, int POL = 0>
+// STAGE (full iterations): 0 the product's (32 window reads, lgkmcnt(0), refill DMA, two compressions);
+// 1 the reads without the wait (the compiler's per-register waits), block 2k-2 hashed, then
+// lgkmcnt(0) and the refill DMA, then block 2k-1; 2 the same with the refill DMA after step 15 of
+// block 2k-2 (md5_compress_hk; MD5 only)
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI, int POL = 0, int STAGE = 0>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const uint8_t *__restrict__ data,
                                                                        uint32_t rec_len, uint64_t n_rec,
                                                                        uint8_t *__restrict__ out, XSplit xs,
@@ -165,11 +249,35 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const ui
     brb_digest::tail_masks(t, tm, tp);
     auto full_step = [&](typename Alg::State &st, const uint32_t (&ad)[32], uint32_t refill_slot) {
         brb_dma::wait_vmcnt<0>();
-        read_window(ad);
-        issue(rs, so, refill_slot);
-        __builtin_amdgcn_sched_barrier(0);
-        Alg::compress(st, w0);
-        Alg::compress(st, w1);
+        if constexpr (STAGE == 0) {
+            read_window(ad);
+            issue(rs, so, refill_slot);
+            __builtin_amdgcn_sched_barrier(0);
+            Alg::compress(st, w0);
+            Alg::compress(st, w1);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                w0[i] = *reinterpret_cast<const uint32_t *>(ring + ad[i]);
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                w1[i] = *reinterpret_cast<const uint32_t *>(ring + ad[16 + i]);
+            __builtin_amdgcn_sched_barrier(0);
+            auto refill = [&]() {
+                __builtin_amdgcn_s_waitcnt(0xC07F);             // every window read has landed
+                issue(rs, so, refill_slot);
+            };
+            if constexpr (STAGE == 1) {
+                Alg::compress(st, w0);
+                __builtin_amdgcn_sched_barrier(0);
+                refill();
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                md5_compress_hk(st, w0, refill);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            Alg::compress(st, w1);
+        }
         __builtin_amdgcn_sched_barrier(0);
     };
     for (;;) {
