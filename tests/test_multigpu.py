@@ -1,4 +1,4 @@
-"""N > 1 path: record sharding with world_size 2 over gloo.
+"""N > 1 path: record sharding with world_size 2 (and 4 on the CPU) over gloo.
 
 Each rank takes a contiguous record range (workload.shard, the same rule as the library's
 BRB_BATCH_ALL_DEVICES split), digests it with the PRODUCT library, and the shards are gathered.  The
@@ -75,13 +75,13 @@ def _worker(rank, world, port, n, L, q, mode):
         dist.destroy_process_group()
 
 
-def _run_sharded(n, mode):
+def _run_sharded(n, mode, world=2):
     import oracle
     L = 1500
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, L, q, mode)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, L, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     full, tmax = q.get(timeout=120)
@@ -90,12 +90,12 @@ def _run_sharded(n, mode):
         assert p.exitcode == 0
     want = oracle.md5_batch_fixed(workload.gen_records(workload.SEEDS[5], 0, n, L), L, n)
     assert np.array_equal(full, want)
-    assert tmax == 2.0
+    assert tmax == float(world)
 
 
-@pytest.mark.parametrize("n", [1000, 1025])
-def test_sharded_compat_digests_equal_unsharded(n):
-    _run_sharded(n, "compat")
+@pytest.mark.parametrize("n,world", [(1000, 2), (1025, 2), (1027, 4)])
+def test_sharded_compat_digests_equal_unsharded(n, world):
+    _run_sharded(n, "compat", world)
 
 
 @pytest.mark.gpu
