@@ -3,7 +3,8 @@
 // 32 ds_read_b32, then lgkmcnt(0) before the refill DMA may overwrite the slot.  Variants of
 // tools/mb/line_xcd_kernel.h at an even split (which times as the product): STAGE 0 (the product's
 // order), 1 (reads, block 2k-2 on the compiler's per-register waits, then the refill DMA, block
-// 2k-1), 2 (the refill DMA after step 15 of block 2k-2).  Digests compared with the product's first.
+// 2k-1), 2 (the refill DMA after step 15 of block 2k-2); and MAP 1 (each workgroup a contiguous block
+// of groups instead of every c_x-th).  Digests compared with the product's first.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -I../../brb_framework_amd/csrc/gpu line_stage.hip -o line_stage
 // Run:   ./line_stage [n_rec=1048576] [rec_len=1500] [rounds=5] [launches=40]
 #include <hip/hip_runtime.h>
@@ -45,6 +46,7 @@ static const void *kx(int v)
     switch (v) {
     case 1: return (const void *)(KX)brb_mb_xcd::digest_line_xcd_kernel<AlgLit, 8, true, HI, 0, 1>;
     case 2: return (const void *)(KX)brb_mb_xcd::digest_line_xcd_kernel<AlgLit, 8, true, HI, 0, 2>;
+    case 3: return (const void *)(KX)brb_mb_xcd::digest_line_xcd_kernel<AlgLit, 8, true, HI, 0, 0, 1>;
     default: return (const void *)(KX)brb_mb_xcd::digest_line_xcd_kernel<AlgLit, 8, true, HI, 0, 0>;
     }
 }
@@ -84,7 +86,7 @@ int main(int argc, char **argv)
             xs.s[k + 1] = uint32_t(groups * acc / grid);
         }
     }
-    const char *names[4] = {"product", "stage0", "stage1 split", "stage2 hook"};
+    const char *names[5] = {"product", "stage0", "stage1 split", "stage2 hook", "blocked groups"};
     auto run = [&](int v, const uint8_t *src) {
         uint64_t nn = n;
         uint32_t LL = L;
@@ -99,7 +101,7 @@ int main(int argc, char **argv)
         }
     };
     std::vector<uint8_t> ref(n * 16), got(n * 16);
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 5; v++) {
         CK(hipMemset(o, 0xA5, n * 16));
         run(v, d[0]);
         CK(hipDeviceSynchronize());
@@ -109,15 +111,15 @@ int main(int argc, char **argv)
             return 2;
         }
     }
-    printf("n=%llu L=%u grid=%u: digests identical across the four variants\n", (unsigned long long)n, L, grid);
+    printf("n=%llu L=%u grid=%u: digests identical across the five variants\n", (unsigned long long)n, L, grid);
     fflush(stdout);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    std::vector<std::vector<double>> us(4);
+    std::vector<std::vector<double>> us(5);
     int it = 0;
     for (int r = 0; r < rounds; r++)
-        for (int v = 0; v < 4; v++) {
+        for (int v = 0; v < 5; v++) {
             float tot = 0;
             while (tot < 300.f) {
                 CK(hipEventRecord(a));
@@ -139,7 +141,7 @@ int main(int argc, char **argv)
                    double(n) * L / (us[v].back() * 1e-6) / 8e12);
             fflush(stdout);
         }
-    for (int v = 0; v < 4; v++)
+    for (int v = 0; v < 5; v++)
         printf("MEDIAN %-12s %.2f us  frac %.4f\n", names[v], med(us[v]), double(n) * L / (med(us[v]) * 1e-6) / 8e12);
     return 0;
 }

@@ -110,7 +110,9 @@ BRB_DEV inline uint64_t rt_now()
 // 1 the reads without the wait (the compiler's per-register waits), block 2k-2 hashed, then
 // lgkmcnt(0) and the refill DMA, then block 2k-1; 2 the same with the refill DMA after step 15 of
 // block 2k-2 (md5_compress_hk; MD5 only)
-template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI, int POL = 0, int STAGE = 0>
+// MAP: 0 workgroup j of a class takes groups g_lo + j + t c_x (interleaved, the product's); 1 it takes
+// a contiguous block of the class's range (the CU's eight waves work on neighbouring groups)
+template <class Alg, int WAVES, bool OUT_ALIGNED, bool TAIL_HI, int POL = 0, int STAGE = 0, int MAP = 0>
 __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const uint8_t *__restrict__ data,
                                                                        uint32_t rec_len, uint64_t n_rec,
                                                                        uint8_t *__restrict__ out, XSplit xs,
@@ -123,7 +125,10 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const ui
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t cls = blockIdx.x & 7, jx = blockIdx.x >> 3;
     const uint32_t cx = (gridDim.x - cls + 7) >> 3;            // workgroups of this class
-    const uint64_t g_lo = xs.s[cls], g_hi = xs.s[cls + 1];
+    const uint64_t c_lo = xs.s[cls], c_hi = xs.s[cls + 1];
+    const uint64_t g_lo = MAP ? c_lo + (uint64_t(jx) * (c_hi - c_lo)) / cx : c_lo;
+    const uint64_t g_hi = MAP ? c_lo + (uint64_t(jx + 1) * (c_hi - c_lo)) / cx : c_hi;
+    const uint64_t g_first = MAP ? g_lo : g_lo + jx, g_step = MAP ? 1 : cx;
     const uint64_t t0 = stamp ? rt_now() : 0;
     if (threadIdx.x == 0)
         next_ticket = WAVES;
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const ui
         if (lane == 0)
             tk = __hip_atomic_fetch_add(&next_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         tk = __builtin_amdgcn_readfirstlane(tk);
-        return g_lo + jx + uint64_t(tk) * cx;
+        return g_first + uint64_t(tk) * g_step;
     };
     auto finish_stamp = [&]() {
         if (stamp && lane == 0) {
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void digest_line_xcd_kernel(const ui
             stamp[3 * w + 2] = xcc;
         }
     };
-    uint64_t g = g_lo + jx + uint64_t(wv) * cx;
+    uint64_t g = g_first + uint64_t(wv) * g_step;
     if (g >= g_hi) {
         finish_stamp();
         return;
