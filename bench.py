@@ -532,6 +532,7 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
         e1.record(streams[0])
         torch.cuda.synchronize()
         barrier()
+        t1 = time.perf_counter()
     finally:
         if gc_was:
             gc.enable()
@@ -539,7 +540,7 @@ def timed_steps(launch, n_steps, streams, barrier, max_over_ranks, torch):
         with torch.cuda.stream(streams[0]):
             torch.cuda._sleep(1)
         torch.cuda.synchronize()
-    wall = max_over_ranks(time.perf_counter() - t0)
+    wall = max_over_ranks(t1 - t0)
     LAST_ALL_K_S = ((ea if steady else e0).elapsed_time(e1) / 1e3 / n_steps) if len(streams) == 1 else None
     return wall, e0.elapsed_time(e1) / 1e3 / (n_steps - 2 if steady else n_steps)
 
