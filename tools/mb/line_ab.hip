@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "digest_line.h"
+#include "line3r_kernel.h"
 #include "line4_kernel.h"
 #include "line_r05_kernel.h"
 #include "md5_device.h"
@@ -39,10 +40,13 @@ struct Var {
     const void *k;
     bool six;     // round-5 signature (pool heads, t_own)
     unsigned threads = 512;
+    bool one_group = false;   // grid = groups / 4 (one group per wave, 4-wave workgroups)
 };
 
 static void launch(const Var &v, unsigned grid, const uint8_t *src, uint32_t L, uint64_t n, uint8_t *o)
 {
+    if (v.one_group)
+        grid = unsigned(((n + 63) / 64 + 3) / 4);
     uint32_t *pool = nullptr;
     uint32_t t_own = 0;
     void *a4[] = {&src, &L, &n, &o};
@@ -81,6 +85,8 @@ int main(int argc, char **argv)
         {"r05 per-group setup", (const void *)(K6)brb_mb_r05::digest_line_kernel<AlgLit, 8, true, true, true>, true},
         {"r06 hoisted", hi ? (const void *)(K4)brb_digest::digest_line_kernel<AlgLit, 8, true, true>
                            : (const void *)(K4)brb_digest::digest_line_kernel<AlgLit, 8, true, false>, false},
+        {"3-slot ring, 1 group/wave", hi ? (const void *)(K4)brb_mb_l3r::digest_line3r_kernel<AlgLit, true, true>
+                                         : (const void *)(K4)brb_mb_l3r::digest_line3r_kernel<AlgLit, true, false>, false, 256, true},
         {"half-line 16 waves", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 16, true>, false, 1024},
         {"half-line 8 waves", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 8, true>, false, 512},
         {"half-line 16 w, all L2", (const void *)(K4)brb_mb_l4::digest_line4_kernel<AlgLit, 16, true, true>, false, 1024},
