@@ -7,6 +7,8 @@ import subprocess
 import sys
 import types
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -89,6 +91,26 @@ def test_timed_steps_multi_stream_brackets_all():
     clock.log.clear()
     _, per1 = bench.timed_steps(launch, 1, ["s0"], lambda: None, lambda x: x, torch)
     assert clock.log == ["event"] * 3 + ["sync", "event", "launch0", "event", "sync"] and abs(per1 - 2.0e-3) < 1e-12
+
+
+def test_timed_steps_restores_gc_when_a_launch_raises():
+    """the collector is off only inside the region; a launch that raises there must not
+    leave it off for the rest of the run (the cfg5 and host-inclusive legs)."""
+    import gc
+
+    clock = _Clock()
+    torch = _fake_torch(clock, 2.0)
+
+    def launch(k, s, j):
+        if k == 2:
+            raise RuntimeError("launch failed")
+        clock.t += 2.0
+
+    bench.MARK = False
+    assert gc.isenabled()
+    with pytest.raises(RuntimeError, match="launch failed"):
+        bench.timed_steps(launch, 5, ["s0"], lambda: None, lambda x: x, torch)
+    assert gc.isenabled()
 
 
 # ---- roofline.traffic / roofline.compute come only from a PMC pass of the timed kernels ------------
